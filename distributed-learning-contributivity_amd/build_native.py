@@ -1,0 +1,83 @@
+"""Build libmplc_hip.so (all HIP kernels + the C ABI of include/mplc_hip.h) for gfx950, in-tree.
+
+    python distributed-learning-contributivity_amd/build_native.py [-v] [--force]
+
+Each csrc/*.hip is compiled to an object with hipcc (parallel, timestamp-checked), then linked into
+mplc/lib/libmplc_hip.so.  The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG_ROOT = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+BUILD = os.path.join(PKG_ROOT, "build")
+LIB_DIR = os.path.join(PKG_ROOT, "mplc", "lib")
+LIB = os.path.join(LIB_DIR, "libmplc_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
+          "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _deps(src):
+    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return [src] + hdrs
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src, obj, verbose):
+    cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, flush=True)
+    return obj
+
+
+def build(verbose=False, force=False, jobs=8):
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    if not srcs:
+        raise RuntimeError("no HIP sources found")
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if force or _stale(o, _deps(s)):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+            list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
+    if force or todo or _stale(LIB, objs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    print(build(verbose=a.verbose, force=a.force))
+    sys.exit(0)

@@ -1,0 +1,99 @@
+/*
+ * mplc_hip.h - C ABI of the MI355X-native MPLC coalition-evaluation engine (libmplc_hip.so).
+ *
+ * The reference (mshuaic/distributed-learning-contributivity, pure Python) has no FFI: its hot path is
+ * Python calling Keras/TF and numpy.  Each entry point below REPLACES one reference interface on the
+ * coalition-evaluation path; the replaced file:line is cited per function.  The Python host package
+ * (distributed-learning-contributivity_amd/mplc) binds these with ctypes (mplc/_native.py).
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless a comment says "host".
+ *  - Buffers are caller-owned.  The library allocates nothing persistent and keeps no pointer after
+ *    return.  Work is enqueued on `stream` (a hipStream_t passed as void*; NULL = default stream);
+ *    nothing synchronises except where stated.
+ *  - Return value: 0 = success; > 0 = hipError_t from a launch; < 0 = MPLC_E_* argument error.
+ *    No function calls exit()/abort().
+ *  - Coalitions are bitmasks: bit i set <=> partner i in S.  v(S) tables are "bitmask order":
+ *    V[mask], mask in [0, 2^n), V[0] = v(empty) = 0 (mplc/contributivity.py:74).
+ */
+#ifndef MPLC_HIP_H
+#define MPLC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPLC_OK 0
+#define MPLC_E_ARG (-1)        /* invalid argument (n out of range, misaligned range, NULL)       */
+#define MPLC_E_WORKSPACE (-2)  /* workspace too small                                            */
+#define MPLC_E_SHAPE (-3)      /* tensor geometry the kernel does not support                    */
+
+/* Version / capability probe: returns MPLC_ABI_VERSION. */
+#define MPLC_ABI_VERSION 1
+int mplc_abi_version(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * Exact Shapley aggregation over the bitmask v(S) table.
+ * Replaces: mplc/contributivity.py:1210-1253 `shapley_value(partners_count, char_func_list)` (pure
+ *           Python, O(n 4^n)) as called from compute_SV mplc/contributivity.py:163.
+ * Formulation (single pass, each V[mask] read once):
+ *   w(s) = s!(n-s-1)!/n!,  A_i = sum_{T contains i} v(T) (w(|T|-1) + w(|T|)),  B = sum_S v(S) w(|S|)
+ *   with w(-1) = w(n) = 0;  SV_i = A_i - B.
+ * Sums are compensated (Kahan in-thread, double-double across threads/blocks).
+ * ---------------------------------------------------------------------------------------------- */
+
+/* Bytes of device workspace mplc_shapley_partial/exact need for `count` masks. */
+size_t mplc_shapley_workspace_bytes(int n, uint64_t count);
+
+/* Partial sums over masks [mask_begin, mask_begin + count) of an n-partner table.
+ * v points at V[mask_begin].  Writes partial_out[2*(n+1)] doubles (device):
+ *   {A_0.hi, A_0.lo, ..., A_{n-1}.hi, A_{n-1}.lo, B.hi, B.lo}.
+ * Partials of disjoint ranges add (hi with hi, lo with lo): the range-sharded multi-GPU form is
+ * partial per rank -> all_reduce(sum) -> mplc_shapley_finalize.
+ * Requirements: 1 <= n <= 40; for n >= 16 mask_begin and count are multiples of 65536. */
+int mplc_shapley_partial(const double* v, uint64_t mask_begin, uint64_t count, int n, double* partial_out,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* sv_out[i] = (A_i.hi - B.hi) + (A_i.lo - B.lo), i < n (device in, device out). */
+int mplc_shapley_finalize(const double* partial, int n, double* sv_out, void* stream);
+
+/* Whole table in one call: partial over [0, 2^n) + finalize.  v has 2^n entries, v[0] ignored (= 0). */
+int mplc_shapley_exact(const double* v, int n, double* sv_out, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * FedAvg weighted partner aggregation, batched over coalitions.
+ * Replaces: mplc/mpl_utils.py:90-102 `Aggregator.aggregate_model_weights` (per-layer
+ *           np.average(stack, axis=0, weights=w) in float64, stored back as float32 by set_weights,
+ *           mplc/multi_partner_learning.py:100-104) for DataVolumeAggregator/UniformAggregator
+ *           (mplc/mpl_utils.py:105-115).
+ * For coalition c with replicas r in [first[c], first[c+1]):
+ *   out[c][k] = float( ( ((double)x[r0][k]*w[r0] + (double)x[r1][k]*w[r1]) + ... ) / scale[c] )
+ * products and sums rounded separately in replica order (numpy's multiply-then-sum, axis 0), then
+ * one division and one fp64->fp32 rounding: bit-identical to the reference's numpy path.
+ * If broadcast != 0 the result is also written into every replica row of the coalition
+ * (x[r][k] = out[c][k]), which starts the next FedAvg round (mplc/multi_partner_learning.py:310-311).
+ * ---------------------------------------------------------------------------------------------- */
+int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, const double* w,
+                          const double* scale, int n_coalitions, int64_t n_param, float* out,
+                          int64_t out_stride, int broadcast, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Batched multi-model MNIST CNN trainer (mplc/dataset.py:457-479 architecture; Keras 2.3.1 Adam).
+ * One "replica" = one (coalition, partner) model.  Replaces, for B replicas at once, the per-partner
+ * Keras `model.fit(x_mb, y_mb, batch_size=bs_p, epochs=1)` of mplc/multi_partner_learning.py:319-332
+ * (FedAvg round), the singleton `model.fit(epochs=E)` of mplc/multi_partner_learning.py:253-260 and
+ * `model.evaluate(x_test, y_test)` of mplc/multi_partner_learning.py:158-169.
+ * Declared in mplc_hip_cnn.h.
+ * ---------------------------------------------------------------------------------------------- */
+
+#ifdef __cplusplus
+}
+#endif
+
+#include "mplc_hip_cnn.h"
+
+#endif /* MPLC_HIP_H */
