@@ -1,0 +1,815 @@
+"""Contributivity measurement - drop-in for mplc/contributivity.py (reference lines cited per method).
+
+The public surface is the reference's: ``Contributivity(scenario, name="")``,
+``compute_contributivity(method_to_compute, sv_accuracy=0.01, alpha=0.95, truncation=0.05, update=50)``,
+``not_twice_characteristic(subset)`` and the result fields (name, contributivity_scores, scores_std,
+normalized_scores, computation_time_sec, first_charac_fct_calls_count, charac_fct_values,
+increments_values).  Estimators consume the global numpy RNG in exactly the reference's order, so on
+a fixed v(S) table every method reproduces the reference bit for bit (tests/test_contributivity.py
+against tests/golden/estimators.json).
+
+What changes is where v(S) comes from.  When the scenario's learning approach is engine-backed (it
+exposes ``evaluate_coalitions``), the estimators first PLAN the coalitions they are about to need and
+have them trained as one batch on the MI355X (exact Shapley: all 2^n - 1; Independent: the n
+singletons; TMCS/ITMCS: the truncation frontier of a wave of speculatively drawn permutations; SMCS /
+WR_SMC / IS: one sampling iteration ahead).  Those values land in a per-scenario coalition cache;
+``not_twice_characteristic`` then runs the reference's memo logic unchanged on top of it, so the memo,
+the increments and ``first_charac_fct_calls_count`` are exactly what the sequential reference records.
+v(S) is a deterministic function of (S, seed) in the engine, so sharing the cache across methods changes
+no result (the reference retrains per method, mplc/scenario.py:872-876, with unseeded TF).
+
+Exact Shapley aggregation runs on device (mplc.shapley, csrc/shapley.hip).
+"""
+import datetime
+import logging
+from itertools import combinations
+from math import factorial
+from timeit import default_timer as timer
+
+import numpy as np
+from scipy.stats import norm
+
+from . import multi_partner_learning, constants
+from .coalitions import tuple_to_mask
+
+logger = logging.getLogger("mplc")
+
+
+# ------------------------------------------------------------------------------------------------
+# Kriging surrogate used by AIS (reference mplc/contributivity.py:22-61)
+# ------------------------------------------------------------------------------------------------
+class KrigingModel:
+    """Universal kriging with polynomial trend in sum(x) of degree `degre` (mplc/contributivity.py:22-61)."""
+
+    def __init__(self, degre, covariance_func):
+        self.degre = degre
+        self.cov_f = covariance_func
+        self.X = np.array([[]])
+        self.Y = np.array([[]])
+        self.beta = np.array([[]])
+        self.H = np.array([[]])
+        self.K = np.array([[]])
+        self.invK = np.array([[]])
+
+    def fit(self, X, Y):
+        self.X, self.Y = X, Y
+        m = len(X)
+        gram = np.zeros((m, m))
+        trend = np.zeros((m, self.degre + 1))
+        for a, xa in enumerate(X):
+            for b, xb in enumerate(X):
+                gram[a, b] = self.cov_f(xa, xb)
+            for d in range(self.degre + 1):
+                trend[a, d] = np.sum(xa) ** d
+        self.H = trend
+        self.K = np.linalg.inv(gram)
+        self.invK = np.linalg.inv(gram)
+        ht_ik_h = trend.transpose().dot(self.invK).dot(trend)
+        self.beta = np.linalg.inv(ht_ik_h).dot(trend.transpose()).dot(self.invK).dot(self.Y)
+
+    def predict(self, x):
+        g = np.array([np.sum(x) ** d for d in range(self.degre + 1)])
+        c = np.array([[self.cov_f(self.X[a], x)] for a in range(len(self.X))])
+        return g.transpose().dot(self.beta) + c.transpose().dot(self.invK).dot(self.Y - self.H.dot(self.beta))
+
+
+def _first_index_above(ratios, u):
+    """Index of the first entry with ratio > u in a non-decreasing cumulative array (the inverse-CDF
+    scans of mplc/contributivity.py:413-422, 785-792), or None if none exceeds u."""
+    i = int(np.searchsorted(ratios, u, side="right"))
+    return i if i < len(ratios) else None
+
+
+class Contributivity:
+    """Per-method contributivity state (mplc/contributivity.py:64-75)."""
+
+    def __init__(self, scenario, name=""):
+        self.name = name
+        self.scenario = scenario
+        nb_partners = len(self.scenario.partners_list)
+        self.contributivity_scores = np.zeros(nb_partners)
+        self.scores_std = np.zeros(nb_partners)
+        self.normalized_scores = np.zeros(nb_partners)
+        self.computation_time_sec = 0.0
+        self.first_charac_fct_calls_count = 0
+        self.charac_fct_values = {(): 0}
+        self.increments_values = [{} for _ in self.scenario.partners_list]
+        self._start = None
+
+    def __str__(self):
+        txt = "\n" + self.name + "\n"
+        txt += "Computation time: " + str(datetime.timedelta(seconds=self.computation_time_sec)) + "\n"
+        txt += "Number of characteristic function computed: " + str(self.first_charac_fct_calls_count) + "\n"
+        txt += f"Contributivity scores: {np.round(self.contributivity_scores, 3)}\n"
+        txt += f"Std of the contributivity scores: {np.round(self.scores_std, 3)}\n"
+        txt += f"Normalized contributivity scores: {np.round(self.normalized_scores, 3)}\n"
+        return txt
+
+    # --------------------------------------------------------------------------------------------
+    # v(S): engine cache + batched planning
+    # --------------------------------------------------------------------------------------------
+    @property
+    def _n(self):
+        return len(self.scenario.partners_list)
+
+    def _batched_evaluator(self):
+        approach = getattr(self.scenario, "multi_partner_learning_approach", None)
+        return getattr(approach, "evaluate_coalitions", None)
+
+    def _cache(self):
+        cache = getattr(self.scenario, "coalition_values", None)
+        if cache is None:
+            cache = {}
+            try:
+                self.scenario.coalition_values = cache
+            except AttributeError:
+                pass
+        return cache
+
+    def prefetch(self, subsets):
+        """Batch-evaluate the not-yet-known coalitions among `subsets` on the engine (no effect on the memo
+        or the call count; those follow the reference's sequential semantics in not_twice_characteristic)."""
+        evaluate = self._batched_evaluator()
+        if evaluate is None:
+            return
+        cache = self._cache()
+        todo, seen = [], set()
+        for s in subsets:
+            key = tuple(sorted(int(i) for i in s))
+            if len(key) == 0 or key in cache or key in self.charac_fct_values or key in seen:
+                continue
+            seen.add(key)
+            todo.append(key)
+        if todo:
+            values = evaluate(self.scenario, todo)
+            for k, v in zip(todo, values):
+                cache[k] = float(v)
+
+    def _coalition_value(self, key):
+        cache = self._cache()
+        if key in cache:
+            return cache[key]
+        if self._batched_evaluator() is not None:
+            self.prefetch([key])
+            return cache[key]
+        # plain approach class: the reference's per-coalition construction (mplc/contributivity.py:100-114)
+        partners = np.array([self.scenario.partners_list[i] for i in key])
+        if len(partners) > 1:
+            mpl = self.scenario.multi_partner_learning_approach(self.scenario, partners_list=partners,
+                                                                is_early_stopping=True, is_save_data=False)
+        else:
+            mpl = multi_partner_learning.SinglePartnerLearning(self.scenario, partner=partners[0],
+                                                               is_early_stopping=True, is_save_data=False)
+        mpl.fit()
+        return mpl.history.score
+
+    def not_twice_characteristic(self, subset):
+        """Memoised v(S) plus the increment bookkeeping of mplc/contributivity.py:92-136."""
+        subset = np.asarray(subset)
+        key = tuple(int(i) for i in np.sort(subset)) if len(subset) > 0 else ()
+        values = self.charac_fct_values
+        if key not in values:
+            self.first_charac_fct_calls_count += 1
+            values[key] = self._coalition_value(key)
+            members = set(key)
+            for i in range(self._n):
+                if i in members:
+                    without = tuple(j for j in key if j != i)
+                    if without in values:
+                        self.increments_values[i][without] = values[key] - values[without]
+                else:
+                    with_i = tuple(sorted(key + (i,)))
+                    if with_i in values:
+                        self.increments_values[i][key] = values[with_i] - values[key]
+        return values[key]
+
+    # --------------------------------------------------------------------------------------------
+    # result helpers
+    # --------------------------------------------------------------------------------------------
+    def _begin(self):
+        self._start = timer()
+
+    def _finish(self, name, scores, std):
+        self.name = name
+        self.contributivity_scores = scores
+        self.scores_std = std
+        self.normalized_scores = self.contributivity_scores / np.sum(self.contributivity_scores)
+        self.computation_time_sec = timer() - self._start
+
+    def _single_partner(self, name, v_all):
+        self._finish(name, np.array([v_all]), np.array([0]))
+
+    def _sizes(self):
+        return [len(p.y_train) for p in self.scenario.partners_list]
+
+    # --------------------------------------------------------------------------------------------
+    # Exact Shapley (mplc/contributivity.py:140-171) and independent scores (:174-192)
+    # --------------------------------------------------------------------------------------------
+    def compute_SV(self):
+        from .shapley import shapley_value
+        self._begin()
+        logger.info("# Launching computation of Shapley Value of all partners")
+        n = self._n
+        coalitions = [list(c) for r in range(1, n + 1) for c in combinations(range(n), r)]
+        self.prefetch(coalitions)
+        char_values = [self.not_twice_characteristic(c) for c in coalitions]
+        sv = shapley_value(n, char_values)
+        self.name = "Shapley"
+        self.contributivity_scores = np.array(sv)
+        self.scores_std = np.zeros(len(sv))
+        self.normalized_scores = sv / np.sum(sv)
+        self.computation_time_sec = timer() - self._start
+
+    def compute_independent_scores(self):
+        self._begin()
+        logger.info("# Launching computation of perf. scores of models trained independently on each partner")
+        n = self._n
+        self.prefetch([(i,) for i in range(n)])
+        scores = [self.not_twice_characteristic(np.array([i])) for i in range(n)]
+        self.name = "Independent scores raw"
+        self.contributivity_scores = np.array(scores)
+        self.scores_std = np.zeros(len(scores))
+        self.normalized_scores = scores / np.sum(scores)
+        self.computation_time_sec = timer() - self._start
+
+    # --------------------------------------------------------------------------------------------
+    # Truncated Monte-Carlo (mplc/contributivity.py:195-253) and interpolated TMC (:257-322)
+    # --------------------------------------------------------------------------------------------
+    def _prefetch_permutation_wave(self, n, v_all, truncation, wave):
+        """Draw the next `wave` permutations WITHOUT consuming the global RNG, walk each one's prefixes up
+        to its truncation point level by level, and batch-evaluate every uncached prefix of a level at
+        once.  These are exactly the coalitions the sequential loop will ask for on those permutations."""
+        if self._batched_evaluator() is None:
+            return
+        state = np.random.get_state()
+        perms = [np.random.permutation(n) for _ in range(wave)]
+        np.random.set_state(state)
+        cache = self._cache()
+        known = self.charac_fct_values
+
+        def value(key):
+            return known[key] if key in known else cache.get(key)
+
+        char_now = [0.0] * wave
+        pos = [0] * wave
+        active = list(range(wave))
+        while active:
+            need = []
+            still = []
+            for w in active:
+                perm = perms[w]
+                while pos[w] < n:
+                    if abs(v_all - char_now[w]) < truncation:
+                        pos[w] = n  # truncated: no further coalition on this permutation
+                        break
+                    key = tuple(sorted(int(i) for i in perm[:pos[w] + 1]))
+                    v = value(key)
+                    if v is None:
+                        need.append(key)
+                        break
+                    char_now[w] = v
+                    pos[w] += 1
+                if pos[w] < n:
+                    still.append(w)
+            if not need:
+                break
+            self.prefetch(need)
+            active = still
+
+    def _truncated_loop(self, n, v_all, sv_accuracy, alpha, truncation, interpolate):
+        rows = np.zeros((128, n))
+        t = 0
+        q = norm.ppf((1 - alpha) / 2, loc=0, scale=1)
+        v_max = 0
+        wave = 0
+        sizes = self._sizes()
+        while t < 100 or t < q ** 2 * v_max / sv_accuracy ** 2:
+            if t >= wave:
+                span = 100 if t < 100 else 50
+                self._prefetch_permutation_wave(n, v_all, truncation, span)
+                wave = t + span
+            t += 1
+            if t > rows.shape[0]:
+                rows = np.vstack((rows, np.zeros_like(rows)))
+            rows[t - 1] = 0.0
+            perm = np.random.permutation(n)
+            chars = np.zeros(n + 1)
+            chars[-1] = v_all
+            slope = None
+            for j in range(n):
+                if abs(v_all - chars[j]) < truncation:
+                    if not interpolate:
+                        chars[j + 1] = chars[j]
+                    else:
+                        if slope is None:
+                            # reference quirk kept: sizes of partners j..n-1 in INDEX order, not permutation
+                            # order (mplc/contributivity.py:297-306)
+                            rest = 0
+                            for i in range(j, n):
+                                rest += sizes[i]
+                            slope = (v_all - chars[j]) / rest
+                        chars[j + 1] = chars[j] + slope * sizes[j]
+                else:
+                    chars[j + 1] = self.not_twice_characteristic(perm[: j + 1])
+                rows[t - 1][perm[j]] = chars[j + 1] - chars[j]
+            v_max = np.max(np.var(rows[:t], axis=0))
+        contributions = rows[:t]
+        return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1)
+
+    def truncated_MC(self, sv_accuracy=0.01, alpha=0.9, truncation=0.05):
+        self._begin()
+        n = self._n
+        v_all = self.not_twice_characteristic(np.arange(n))
+        if n == 1:
+            return self._single_partner("TMC Shapley", v_all)
+        sv, std = self._truncated_loop(n, v_all, sv_accuracy, alpha, truncation, interpolate=False)
+        self._finish("TMC Shapley", sv, std)
+
+    def interpol_TMC(self, sv_accuracy=0.01, alpha=0.9, truncation=0.05):
+        self._begin()
+        n = self._n
+        v_all = self.not_twice_characteristic(np.arange(n))
+        if n == 1:
+            return self._single_partner("ITMCS", v_all)
+        sv, std = self._truncated_loop(n, v_all, sv_accuracy, alpha, truncation, interpolate=True)
+        self._finish("ITMCS", sv, std)
+
+    # --------------------------------------------------------------------------------------------
+    # Importance sampling (mplc/contributivity.py:326-439 linear, :443-569 regression)
+    # --------------------------------------------------------------------------------------------
+    def _prob(self, n, size):
+        return factorial(n - 1 - size) * factorial(size) / factorial(n)
+
+    def _importance_tables(self, n, approx_for):
+        """Per player k: the combination-ordered subsets of the others and the running cumSum / renorm
+        ratios of the reference's inverse-CDF scan (same sequential sums, mplc/contributivity.py:380-393)."""
+        tables = []
+        renorms = []
+        for k in range(n):
+            others = [i for i in range(n) if i != k]
+            subsets, cums = [], []
+            acc = 0
+            for length in range(len(others) + 1):
+                for sub in combinations(others, length):
+                    acc += self._prob(n, len(sub)) * np.abs(approx_for(sub, k))
+                    subsets.append(sub)
+                    cums.append(acc)
+            renorms.append(acc)
+            tables.append((subsets, np.asarray(cums, dtype=np.float64) / acc if acc != 0 else np.full(len(cums), np.nan)))
+        return tables, renorms
+
+    def _importance_loop(self, n, sv_accuracy, alpha, tables, renorms, approx_for):
+        q = -norm.ppf((1 - alpha) / 2, loc=0, scale=1)
+        rows = np.zeros((128, n))
+        t = 0
+        v_max = 0
+        S = None
+        while t < 100 or t < 4 * q ** 2 * v_max / sv_accuracy ** 2:
+            t += 1
+            if t > rows.shape[0]:
+                rows = np.vstack((rows, np.zeros_like(rows)))
+            rows[t - 1] = 0.0
+            # plan this iteration's draws on a copy of the RNG, batch the needed coalitions
+            if self._batched_evaluator() is not None:
+                state = np.random.get_state()
+                plan = []
+                for k in range(n):
+                    u = np.random.uniform(0, 1, 1)[0]
+                    idx = _first_index_above(tables[k][1], u)
+                    if idx is not None:
+                        sub = tables[k][0][idx]
+                        plan += [tuple(sorted(sub + (k,))), sub]
+                np.random.set_state(state)
+                self.prefetch(plan)
+            for k in range(n):
+                u = np.random.uniform(0, 1, 1)[0]
+                idx = _first_index_above(tables[k][1], u)
+                if idx is not None:
+                    S = np.array(tables[k][0][idx])
+                if S is None:
+                    raise UnboundLocalError("local variable 'S' referenced before assignment")
+                SUk = np.append(S, k)
+                increment = self.not_twice_characteristic(SUk) - self.not_twice_characteristic(S)
+                rows[t - 1][k] = increment * renorms[k] / np.abs(approx_for(tuple(int(i) for i in S), k))
+            v_max = np.max(np.var(rows[:t], axis=0))
+        contributions = rows[:t]
+        return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1)
+
+    def IS_lin(self, sv_accuracy=0.01, alpha=0.95):
+        self._begin()
+        n = self._n
+        v_all = self.not_twice_characteristic(np.arange(n))
+        if n == 1:
+            return self._single_partner("IS_lin Shapley", v_all)
+        self.prefetch([tuple(i for i in range(n) if i != k) for k in range(n)] + [(k,) for k in range(n)])
+        last_inc, first_inc = [], []
+        for k in range(n):
+            last_inc.append(v_all - self.not_twice_characteristic(np.delete(np.arange(n), k)))
+            first_inc.append(self.not_twice_characteristic(np.array([k])) - 0)
+        sizes = self._sizes()
+        size_all = 0
+        for s in sizes:
+            size_all += s
+        memo = {}
+
+        def approx_for(sub, k):
+            # depends on sum of sizes only (mplc/contributivity.py:369-377)
+            size_S = 0
+            for i in sub:
+                size_S += sizes[i]
+            key = (size_S, k)
+            if key not in memo:
+                beta = size_S / size_all
+                memo[key] = (1 - beta) * first_inc[k] + beta * last_inc[k]
+            return memo[key]
+
+        tables, renorms = self._importance_tables(n, approx_for)
+        sv, std = self._importance_loop(n, sv_accuracy, alpha, tables, renorms, approx_for)
+        self._finish("IS_lin Shapley", sv, std)
+
+    def IS_reg(self, sv_accuracy=0.01, alpha=0.95):
+        from sklearn.linear_model import LinearRegression
+        self._begin()
+        n = self._n
+        if n < 4:
+            self.compute_SV()
+            self.name = "IS_reg Shapley values"
+            return
+        # seed increments along 2 + n rotated permutations (mplc/contributivity.py:462-472)
+        perm = np.random.permutation(n)
+        walks = [perm, np.flip(perm)]
+        p = walks[-1]
+        for _ in range(n):
+            p = np.append(p[-1], p[:-1])
+            walks.append(p)
+        self.prefetch([tuple(sorted(int(i) for i in w[: j + 1])) for w in walks for j in range(n)])
+        for w in walks:
+            for j in range(n):
+                self.not_twice_characteristic(w[: j + 1])
+        sizes = self._sizes()
+
+        def features(sub):
+            size_S = 0
+            for i in sub:
+                size_S += sizes[i]
+            return [size_S, size_S ** 2]
+
+        models = []
+        for k in range(n):
+            X = [features(sub) for sub in self.increments_values[k]]
+            y = list(self.increments_values[k].values())
+            models.append(LinearRegression().fit(X, y))
+        memo = {}
+
+        def approx_for(sub, k):
+            f = features(sub)
+            key = (f[0], k)
+            if key not in memo:
+                memo[key] = models[k].predict([f])[0]
+            return memo[key]
+
+        tables, renorms = self._importance_tables(n, approx_for)
+        sv, std = self._importance_loop(n, sv_accuracy, alpha, tables, renorms, approx_for)
+        self._finish("IS_reg Shapley", sv, std)
+
+    # --------------------------------------------------------------------------------------------
+    # Adaptive importance sampling with Kriging (mplc/contributivity.py:573-723)
+    # --------------------------------------------------------------------------------------------
+    def AIS_Kriging(self, sv_accuracy=0.01, alpha=0.95, update=50):
+        self._begin()
+        n = self._n
+        full = np.arange(n)
+        seeds = [tuple(range(n))]
+        for k1 in range(n):
+            for k2 in range(n):
+                seeds += [(k1,), tuple(np.delete(full, [k1]))]
+                if k1 != k2:
+                    seeds += [tuple(sorted((k1, k2))), tuple(np.delete(full, [k1, k2]))]
+        self.prefetch(seeds)
+        self.not_twice_characteristic(full)
+        for k1 in range(n):
+            for k2 in range(n):
+                self.not_twice_characteristic(np.array([k1]))
+                self.not_twice_characteristic(np.delete(full, [k1]))
+                if k1 != k2:
+                    self.not_twice_characteristic(np.array([k1, k2]))
+                    self.not_twice_characteristic(np.delete(full, [k1, k2]))
+        sizes = self._sizes()
+
+        def coordinate(sub, k):
+            c = np.zeros(n)
+            for i in sub:
+                c[i] = sizes[i]
+            return np.delete(c, k)
+
+        phi = np.zeros(n)
+        for k in range(n):
+            phi[k] = np.median(coordinate(np.delete(full, k), k))
+
+        # Reference closure quirk (mplc/contributivity.py:618-624): each covk reads phi[k] through the
+        # late-bound loop variable k of AIS_Kriging's own scope, i.e. the k of whatever loop is running
+        # when the covariance is evaluated: n - 1 while models are fitted, the current player while the
+        # renormalisation and sampling loops predict.  `live_k` reproduces that binding.
+        live_k = [n - 1]
+
+        def cov(x1, x2):
+            return np.exp(-np.sqrt(np.sum((x1 - x2) ** 2)) ** 2 / phi[live_k[0]] ** 2)
+
+        generations = []
+        gen_tables = []
+
+        def refit():
+            models = []
+            for k in range(n):
+                X = [coordinate(sub, k) for sub in self.increments_values[k]]
+                Y = [v for v in self.increments_values[k].values()]
+                m = KrigingModel(2, cov)
+                m.fit(X, Y)
+                models.append(m)
+            generations.append(models)
+
+        q = -norm.ppf((1 - alpha) / 2, loc=0, scale=1)
+        t = 0
+        v_max = 0
+        contributions = None
+        S = None
+        j = 0
+        while t < 100 or t < 4 * q ** 2 * v_max / sv_accuracy ** 2:
+            if t == 0:
+                contributions = np.array([np.zeros(n)])
+            else:
+                contributions = np.vstack((contributions, np.zeros(n)))
+            if t % update == 0:
+                j = t // update
+                live_k[0] = n - 1
+                refit()
+                memo = {}
+
+                def approx_for(sub, k, _models=generations[j], _memo=memo):
+                    key = (tuple(sub), k)
+                    if key not in _memo:
+                        live_k[0] = k
+                        _memo[key] = _models[k].predict(coordinate(sub, k))[0]
+                    return _memo[key]
+
+                tables, renorms = self._importance_tables(n, approx_for)
+                gen_tables.append((tables, renorms, approx_for))
+            tables, renorms, approx_for = gen_tables[j]
+            if self._batched_evaluator() is not None:
+                state = np.random.get_state()
+                plan = []
+                for k in range(n):
+                    idx = _first_index_above(tables[k][1], np.random.uniform(0, 1, 1)[0])
+                    if idx is not None:
+                        plan += [tuple(sorted(tables[k][0][idx] + (k,))), tables[k][0][idx]]
+                np.random.set_state(state)
+                self.prefetch(plan)
+            for k in range(n):
+                u = np.random.uniform(0, 1, 1)[0]
+                idx = _first_index_above(tables[k][1], u)
+                if idx is not None:
+                    S = np.array(tables[k][0][idx])
+                if S is None:
+                    raise UnboundLocalError("local variable 'S' referenced before assignment")
+                SUk = np.append(S, k)
+                increment = self.not_twice_characteristic(SUk) - self.not_twice_characteristic(S)
+                # reference indexing kept: row t - 1 (the last row at t = 0) (mplc/contributivity.py:709)
+                contributions[t - 1][k] = increment * renorms[k] / np.abs(approx_for(tuple(int(i) for i in S), k))
+            v_max = np.max(np.var(contributions, axis=0))
+            t += 1
+        self._finish("AIS Shapley", np.mean(contributions, axis=0),
+                     np.std(contributions, axis=0) / np.sqrt(t - 1))
+
+    # --------------------------------------------------------------------------------------------
+    # Stratified MC (mplc/contributivity.py:727-819) and without-replacement SMC (:823-938)
+    # --------------------------------------------------------------------------------------------
+    def _stratum_cdf(self, N, strata):
+        """cumSum after each combination of one stratum, added sequentially (mplc/contributivity.py:786-792)."""
+        cache = getattr(self, "_cdf_cache", None)
+        if cache is None:
+            cache = self._cdf_cache = {}
+        key = (N, strata)
+        if key not in cache:
+            step = factorial(N - 1 - strata) * factorial(strata) / factorial(N - 1)
+            count = factorial(N - 1) // (factorial(N - 1 - strata) * factorial(strata))
+            vals = np.empty(count)
+            acc = 0
+            for i in range(count):
+                acc += step
+                vals[i] = acc
+            cache[key] = vals
+        return cache[key]
+
+    @staticmethod
+    def _unrank_combination(items, size, rank):
+        """The rank-th combination (lexicographic, as itertools.combinations) of `size` elements of items."""
+        out = []
+        m = len(items)
+        start = 0
+        for slot in range(size):
+            for i in range(start, m):
+                block = _binom(m - i - 1, size - slot - 1)
+                if rank < block:
+                    out.append(items[i])
+                    start = i + 1
+                    break
+                rank -= block
+        return tuple(out)
+
+    def _stratified_pick(self, N, k, strata, u):
+        cdf = self._stratum_cdf(N, strata)
+        idx = _first_index_above(cdf, u)
+        if idx is None:
+            return None
+        others = [i for i in range(N) if i != k]
+        return self._unrank_combination(others, strata, idx)
+
+    def Stratified_MC(self, sv_accuracy=0.01, alpha=0.95):
+        self._begin()
+        N = self._n
+        v_all = self.not_twice_characteristic(np.arange(N))
+        if N == 1:
+            return self._single_partner("Stratified MC Shapley", v_all)
+        gamma, beta = 0.2, 0.0075
+        t = 0
+        sigma2 = np.zeros((N, N))
+        mu = np.zeros((N, N))
+        v_max = 0
+        keep_going = [[True] * N for _ in range(N)]
+        samples = [[[] for _ in range(N)] for _ in range(N)]
+        S = None
+        var = np.zeros(N)
+        while np.any(keep_going) or (1 - alpha) < v_max / (sv_accuracy ** 2):
+            t += 1
+            e = 1 + 1 / (1 + np.exp(gamma / beta)) - 1 / (1 + np.exp(-(t - gamma * N) / (beta * N)))
+
+            def alloc(k):
+                if np.sum(sigma2[k]) == 0:
+                    return np.repeat(1 / N, N)
+                return np.repeat(1 / N, N) * (1 - e) + sigma2[k] / np.sum(sigma2[k]) * e
+
+            # within one iteration the draws of player k depend only on sigma2[k] from earlier iterations
+            if self._batched_evaluator() is not None:
+                state = np.random.get_state()
+                plan = []
+                for k in range(N):
+                    st = np.random.choice(np.arange(N), 1, p=alloc(k))[0]
+                    sub = self._stratified_pick(N, k, st, np.random.uniform(0, 1, 1)[0])
+                    if sub is not None:
+                        plan += [tuple(sorted(sub + (k,))), sub]
+                np.random.set_state(state)
+                self.prefetch(plan)
+            for k in range(N):
+                strata = np.random.choice(np.arange(N), 1, p=alloc(k))[0]
+                u = np.random.uniform(0, 1, 1)[0]
+                sub = self._stratified_pick(N, k, strata, u)
+                if sub is not None:
+                    S = np.array(sub, dtype=int)
+                if S is None:
+                    raise UnboundLocalError("local variable 'S' referenced before assignment")
+                SUk = np.append(S, k)
+                increment = self.not_twice_characteristic(SUk) - self.not_twice_characteristic(S)
+                samples[k][strata].append(increment)
+                sigma2[k, strata] = np.var(samples[k][strata])
+                mu[k, strata] = np.mean(samples[k][strata])
+            shap = np.mean(mu, axis=1)
+            var = np.zeros(N)
+            for k in range(N):
+                for strata in range(N):
+                    cnt = len(samples[k][strata])
+                    if cnt == 0:
+                        var[k] = np.inf
+                    else:
+                        var[k] += sigma2[k, strata] ** 2 / cnt  # sigma2 squared: reference quirk (:809)
+                    if cnt > 20:
+                        keep_going[k][strata] = False
+                var[k] /= N ** 2
+            v_max = np.max(var)
+        self._finish("Stratified MC Shapley", shap, np.sqrt(var))
+
+    def without_replacment_SMC(self, sv_accuracy=0.01, alpha=0.95):
+        self._begin()
+        N = self._n
+        v_all = self.not_twice_characteristic(np.arange(N))
+        if N == 1:
+            return self._single_partner("WR_SMC Shapley", v_all)
+        t = 0
+        sigma2 = np.zeros((N, N))
+        mu = np.zeros((N, N))
+        v_max = 0
+        keep_going = [[True] * N for _ in range(N)]
+        drawn = [[dict() for _ in range(N)] for _ in range(N)]
+        pending = []
+        for k in range(N):
+            others = [i for i in range(N) if i != k]
+            pending.append([list(combinations(others, strata)) for strata in range(N)])
+        var = np.zeros(N)
+        while np.any(keep_going) or (1 - alpha) < v_max / (sv_accuracy ** 2):
+            t += 1
+
+            def alloc(k):
+                if np.any(keep_going[k]):
+                    return np.array(keep_going[k]) / np.sum(keep_going[k])
+                if np.sum(sigma2[k]) == 0:
+                    return None
+                return sigma2[k] / np.sum(sigma2[k])
+
+            if self._batched_evaluator() is not None:
+                state = np.random.get_state()
+                plan = []
+                for k in range(N):
+                    p = alloc(k)
+                    if p is None:
+                        continue
+                    st = np.random.choice(np.arange(N), 1, p=p)[0]
+                    L = len(pending[k][st])
+                    sub = pending[k][st][np.random.choice(L, 1, p=np.repeat(1 / L, L))[0]]
+                    plan += [tuple(sorted(sub + (k,))), sub]
+                np.random.set_state(state)
+                self.prefetch(plan)
+            for k in range(N):
+                p = alloc(k)
+                if p is None:
+                    continue
+                strata = np.random.choice(np.arange(N), 1, p=p)[0]
+                L = len(pending[k][strata])
+                pick = np.random.choice(L, 1, p=np.repeat(1 / L, L))[0]
+                sub = pending[k][strata].pop(pick)
+                S = np.array(list(sub), dtype=int)
+                SUk = np.append(S, k)
+                increment = self.not_twice_characteristic(SUk) - self.not_twice_characteristic(S)
+                drawn[k][strata][sub] = increment
+                L = len(drawn[k][strata])
+                mu[k, strata] = (mu[k, strata] * (L - 1) + increment) / L
+                sigma2[k, strata] = 0
+                for v in drawn[k][strata].values():
+                    sigma2[k, strata] += (v - mu[k, strata]) ** 2
+                if L > 1:
+                    sigma2[k, strata] /= L - 1
+                else:
+                    sigma2[k, strata] = 0
+                sigma2[k, strata] *= 1 / L - factorial(N - 1 - strata) * factorial(strata) / factorial(N - 1)
+            shap = np.mean(mu, axis=1)
+            var = np.zeros(N)
+            for k in range(N):
+                for strata in range(N):
+                    cnt = len(drawn[k][strata])
+                    if cnt == 0:
+                        var[k] = np.inf
+                    else:
+                        var[k] += sigma2[k, strata] ** 2 / cnt
+                    if cnt > 20:
+                        keep_going[k][strata] = False
+                    if len(drawn[k][strata]) == factorial(N - 1) / (factorial(N - 1 - strata) * factorial(strata)):
+                        keep_going[k][strata] = False
+                var[k] /= N ** 2
+            v_max = np.max(var)
+        self._finish("WR_SMC Shapley", shap, np.sqrt(var))
+
+    # --------------------------------------------------------------------------------------------
+    # Dispatcher (mplc/contributivity.py:1134-1198)
+    # --------------------------------------------------------------------------------------------
+    OUT_OF_SCOPE = ("Federated SBS linear", "Federated SBS quadratic", "Federated SBS constant", "PVRL", "LFlip")
+
+    def compute_contributivity(self, method_to_compute, sv_accuracy=0.01, alpha=0.95, truncation=0.05,
+                               update=50):
+        dispatch = {
+            "Shapley values": lambda: self.compute_SV(),
+            "Independent scores": lambda: self.compute_independent_scores(),
+            "TMCS": lambda: self.truncated_MC(sv_accuracy=sv_accuracy, alpha=alpha, truncation=truncation),
+            "ITMCS": lambda: self.interpol_TMC(sv_accuracy=sv_accuracy, alpha=alpha, truncation=truncation),
+            "IS_lin_S": lambda: self.IS_lin(sv_accuracy=sv_accuracy, alpha=alpha),
+            "IS_reg_S": lambda: self.IS_reg(sv_accuracy=sv_accuracy, alpha=alpha),
+            "AIS_Kriging_S": lambda: self.AIS_Kriging(sv_accuracy=sv_accuracy, alpha=alpha, update=update),
+            "SMCS": lambda: self.Stratified_MC(sv_accuracy=sv_accuracy, alpha=alpha),
+            "WR_SMC": lambda: self.without_replacment_SMC(sv_accuracy=sv_accuracy, alpha=alpha),
+        }
+        if method_to_compute in dispatch:
+            dispatch[method_to_compute]()
+        elif method_to_compute in self.OUT_OF_SCOPE:
+            raise NotImplementedError(
+                f"'{method_to_compute}' makes no coalition evaluations (it post-processes one learning history, "
+                "or is broken in the reference); it is outside this engine's scope (DESIGN.md)")
+        else:
+            logger.warning("Unrecognized name of method, statement ignored!")
+
+
+def _binom(a, b):
+    if b < 0 or b > a:
+        return 0
+    return factorial(a) // (factorial(b) * factorial(a - b))
+
+
+__all__ = ["Contributivity", "KrigingModel", "constants"]
+
+# keep the reference's module-level names importable
+from .shapley import shapley_value  # noqa: E402,F401
+
+
+def power_set(List):
+    """mplc/contributivity.py:1205-1207."""
+    return [list(j) for i in range(len(List)) for j in combinations(List, i + 1)]
+
+
+def coalition_mask(subset):
+    return tuple_to_mask(subset)

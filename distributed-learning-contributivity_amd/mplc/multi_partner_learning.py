@@ -1,0 +1,109 @@
+"""Multi-partner learning approaches - drop-in for mplc/multi_partner_learning.py on the coalition path.
+
+The reference trains one Keras model per partner per round, one coalition at a time
+(mplc/multi_partner_learning.py:195-334).  Here the approach classes keep the reference's constructor
+and ``fit()`` / ``history.score`` contract (used by Contributivity.not_twice_characteristic,
+mplc/contributivity.py:100-114) but delegate to the scenario's batched MI355X engine
+(mplc/engine.py), and additionally expose ``evaluate_coalitions(scenario, coalitions)`` so that
+contributivity estimators can have many coalitions trained at once.
+"""
+import operator
+from timeit import default_timer as timer
+
+import numpy as np
+
+from . import constants
+
+ALLOWED_PARAMETERS = ('partners_list', 'epoch_count', 'minibatch_count', 'dataset', 'aggregation_method',
+                      'is_early_stopping', 'is_save_data', 'save_folder', 'init_model_from', 'use_saved_weights')
+
+
+class History:
+    """Subset of mplc/mpl_utils.py:11-27 that the coalition path reads: score and nb_epochs_done."""
+
+    def __init__(self):
+        self.score = None
+        self.nb_epochs_done = 0
+        self.history = {}
+
+
+def _engine(scenario):
+    eng = getattr(scenario, "engine", None)
+    if eng is None:
+        from .engine import CoalitionEngine
+        eng = CoalitionEngine.for_scenario(scenario)
+        scenario.engine = eng
+    return eng
+
+
+class MultiPartnerLearning:
+    """Common constructor (mplc/multi_partner_learning.py:34-91): attributes come from the scenario and
+    may be overridden by ALLOWED_PARAMETERS kwargs."""
+
+    def __init__(self, scenario, **kwargs):
+        self.scenario = scenario
+        self.dataset = getattr(scenario, "dataset", None)
+        self.partners_list = scenario.partners_list
+        self.epoch_count = getattr(scenario, "epoch_count", constants.DEFAULT_EPOCH_COUNT)
+        self.minibatch_count = getattr(scenario, "minibatch_count", constants.DEFAULT_BATCH_COUNT)
+        self.is_early_stopping = getattr(scenario, "is_early_stopping", True)
+        self.aggregation_method = getattr(scenario, "aggregation", None)
+        self.is_save_data = False
+        self.save_folder = getattr(scenario, "save_folder", None)
+        self.__dict__.update((k, v) for k, v in kwargs.items() if k in ALLOWED_PARAMETERS)
+        for partner in self.partners_list:
+            if not hasattr(partner, "id"):
+                raise TypeError("partners_list must hold Partner objects")
+        self.epoch_index = 0
+        self.minibatch_index = 0
+        self.learning_computation_time = 0
+        self.history = History()
+
+    @property
+    def partners_count(self):
+        return len(self.partners_list)
+
+    def _coalition(self):
+        return tuple(sorted(int(p.id) for p in self.partners_list))
+
+    def fit(self):
+        start = timer()
+        eng = _engine(self.scenario)
+        res = eng.evaluate([self._coalition()], epoch_count=self.epoch_count,
+                           is_early_stopping=self.is_early_stopping, return_details=True)
+        self.history.score = float(res["scores"][0])
+        self.history.nb_epochs_done = int(res["epochs_done"][0])
+        self.learning_computation_time = timer() - start
+
+    @classmethod
+    def evaluate_coalitions(cls, scenario, coalitions):
+        """Batched v(S) for many coalitions (test accuracy of the trained coalition model), float64 array."""
+        return _engine(scenario).evaluate(list(coalitions))
+
+
+class SinglePartnerLearning(MultiPartnerLearning):
+    """mplc/multi_partner_learning.py:230-275: one model, fit(epochs=E, bs=partner.batch_size)."""
+
+    def __init__(self, scenario, partner, **kwargs):
+        if type(partner) == list:
+            raise ValueError('More than one partner is provided')
+        kwargs['partners_list'] = [partner]
+        super().__init__(scenario, **kwargs)
+        self.partner = partner
+
+
+class FederatedAverageLearning(MultiPartnerLearning):
+    """mplc/multi_partner_learning.py:278-334: FedAvg rounds over minibatches, fresh optimizer per partner fit."""
+
+    def __init__(self, scenario, **kwargs):
+        super().__init__(scenario, **kwargs)
+        if self.partners_count == 1:
+            raise ValueError('Only one partner is provided. Please use the dedicated SinglePartnerLearning class')
+
+
+MULTI_PARTNER_LEARNING_APPROACHES = {
+    "fedavg": FederatedAverageLearning,
+}
+
+__all__ = ["MultiPartnerLearning", "SinglePartnerLearning", "FederatedAverageLearning",
+           "MULTI_PARTNER_LEARNING_APPROACHES", "operator", "np"]
