@@ -1,0 +1,900 @@
+// Batched multi-model MNIST CNN trainer for gfx950 (see include/mplc_hip_cnn.h for the contract).
+//
+// One lockstep step of B replicas = 9 launches:
+//   schedule        per replica: this step's sample rows, batch count, Adam step     (index work)
+//   conv_fwd        conv1 (recomputed, VALU) -> conv2 implicit GEMM on fp32 MFMA 32x32x2 -> +b, ReLU,
+//                   2x2 max-pool fused in the accumulator layout -> pooled + argmax code
+//   dense_fwd       Dense(128)+ReLU: per-replica GEMM [b x 9216] x [9216 x 128], fp32 MFMA
+//   head            Dense(10), softmax-CE gradient, dW4/db4 + Adam, dh = dlogits W4^T * relu'
+//   dense1_bwd_adam per 64-row slice of W3: dp = dh W3^T, dW3 = p^T dh, Adam(W3) in the same pass
+//                   (W3 = 98% of the parameters: read once, written once per step)
+//   transpose_w2    W2 [kyx][ci][co] -> [kyx][co][ci] for coalesced MFMA B-fragments in the dgrad
+//   conv_bwd_data   dA1 = dZ2 (*) W2 on MFMA, dZ2 rebuilt on the fly from (dp, argmax code); ReLU' of
+//                   the recomputed conv1 output and conv1's weight gradient fused in the epilogue
+//   conv_wgrad      dW2 = A1^T dZ2 on MFMA over all pixels of a replica's samples (split-K partials)
+//   adam_small      Adam on W1/b1/W2/b2 from the per-sample / per-split partials (fixed order: bitwise
+//                   reproducible)
+// Everything is fp32 (the reference's Keras float32), accumulation on the exact-f32 MFMA.
+// conv1's output (86.5 KB/sample) is never written to HBM: it is recomputed (9 MACs/element) by the
+// three kernels that need it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mplc_hip.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int IMG = 28;
+constexpr int A1 = 26;
+constexpr int C1 = 32;
+constexpr int Z2 = 24;
+constexpr int C2 = 64;
+constexpr int PL = 12;
+constexpr int FEAT = 9216;
+constexpr int HID = 128;
+constexpr int NCLS = 10;
+constexpr int64_t OFF_W1 = MPLC_CNN_OFF_W1, OFF_B1 = MPLC_CNN_OFF_B1, OFF_W2 = MPLC_CNN_OFF_W2,
+                  OFF_B2 = MPLC_CNN_OFF_B2, OFF_W3 = MPLC_CNN_OFF_W3, OFF_B3 = MPLC_CNN_OFF_B3,
+                  OFF_W4 = MPLC_CNN_OFF_W4, OFF_B4 = MPLC_CNN_OFF_B4;
+constexpr int A1P = 33;  // padded channel stride of conv1 output tiles in LDS (bank-conflict-free A reads)
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.0f;
+  return z;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Keyed index permutations (bit-identical restatement in oracle/cnn.py)
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t subkey(uint64_t key, uint32_t a, uint32_t b) {
+  return mix64(key ^ mix64(((uint64_t)a << 32) | (uint64_t)b));
+}
+
+// Bijection of [0, n) (balanced 4-round Feistel on 2h bits + cycle walking).
+__device__ __forceinline__ uint32_t keyed_perm(uint64_t key, uint32_t n, uint32_t i) {
+  if (n <= 1) return 0;
+  int bits = 32 - __clz(n - 1);  // ceil(log2 n)
+  const int h = (bits + 1) >> 1;
+  const uint32_t mask = (1u << h) - 1u;
+  uint32_t x = i;
+  do {
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int rd = 0; rd < 4; ++rd) {
+      const uint32_t F = (uint32_t)mix64(key ^ ((uint64_t)rd << 40) ^ (uint64_t)R) & mask;
+      const uint32_t nl = R;
+      R = L ^ F;
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Initialisation: glorot_uniform kernels (Keras default), zero biases / padding.
+// u = top 24 bits of mix64(key + i*golden) / 2^24;  w = (2u - 1) * limit  (fp32, exact restatable)
+// ------------------------------------------------------------------------------------------------
+__global__ void init_params_kernel(float* __restrict__ params, int64_t stride, const uint64_t* __restrict__ keys) {
+  const int m = blockIdx.y;
+  const uint64_t key = keys[m];
+  float* row = params + (int64_t)m * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += (int64_t)gridDim.x * blockDim.x) {
+    float lim = 0.0f;
+    int64_t li = 0;
+    if (i < OFF_B1) { lim = 0x1.23170ep-3f; li = i - OFF_W1; }
+    else if (i >= OFF_W2 && i < OFF_B2) { lim = 0x1.555556p-4f; li = i - OFF_W2; }
+    else if (i >= OFF_W3 && i < OFF_B3) { lim = 0x1.9f2c4cp-6f; li = i - OFF_W3; }
+    else if (i >= OFF_W4 && i < OFF_B4) { lim = 0x1.ab099ap-3f; li = i - OFF_W4; }
+    float w = 0.0f;
+    if (lim != 0.0f) {
+      const uint64_t hsh = mix64(key + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+      const float u = (float)(uint32_t)(hsh >> 40) * 0x1p-24f;
+      w = (u * 2.0f - 1.0f) * lim;
+    }
+    (void)li;
+    row[i] = w;
+  }
+}
+
+__global__ void copy_rows_kernel(float* __restrict__ dst, const float* __restrict__ src, int64_t stride,
+                                 const int32_t* __restrict__ map) {
+  const int r = blockIdx.y;
+  const float4* s = reinterpret_cast<const float4*>(src + (int64_t)map[r] * stride);
+  float4* d = reinterpret_cast<float4*>(dst + (int64_t)r * stride);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride / 4; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = s[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Schedule: global step -> per-replica sample rows (reference sample order, keyed permutations)
+// ------------------------------------------------------------------------------------------------
+__global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_rep, int bmax,
+                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits, int step,
+                                int M, int round_len, int epochs, int32_t* __restrict__ idx,
+                                int32_t* __restrict__ cnt, int32_t* __restrict__ adam_t) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)n_rep * bmax) return;
+  const int r = (int)(gid / bmax);
+  const int j = (int)(gid % bmax);
+  const mplc_replica_t rep = reps[r];
+  int c = 0, at = 0, row = -1;
+  if (rep.kind == MPLC_REP_FEDAVG) {
+    const int per_epoch = M * round_len;
+    const int e = step / per_epoch;
+    const int rem = step % per_epoch;
+    const int m = rem / round_len;
+    const int t = rem % round_len;
+    if (e < epochs) {
+      const int s0 = splits[rep.split_off + m];
+      const int s1 = splits[rep.split_off + m + 1];
+      const int L = s1 - s0;
+      const int nsteps = (L + rep.batch - 1) / rep.batch;
+      if (t < nsteps) {
+        c = min(rep.batch, L - t * rep.batch);
+        at = t + 1;
+        if (j < c) {
+          // Keras fit shuffle inside minibatch m, then the epoch permutation of split_minibatches
+          const uint32_t q = keyed_perm(subkey(rep.key, 0x20000u + (uint32_t)e, (uint32_t)m), (uint32_t)L,
+                                        (uint32_t)(t * rep.batch + j));
+          const uint32_t pos = keyed_perm(subkey(rep.key, 0x10000u + (uint32_t)e, 0u), (uint32_t)rep.n_rows,
+                                          (uint32_t)s0 + q);
+          row = rows[rep.rows_off + (int)pos];
+        }
+      }
+    }
+  } else if (rep.kind == MPLC_REP_SINGLE) {
+    const int spe = (rep.n_rows + rep.batch - 1) / rep.batch;
+    const int e = step / spe;
+    const int t = step % spe;
+    if (e < epochs) {
+      c = min(rep.batch, rep.n_rows - t * rep.batch);
+      at = step + 1;
+      if (j < c) {
+        const uint32_t pos = keyed_perm(subkey(rep.key, 0x30000u + (uint32_t)e, 0u), (uint32_t)rep.n_rows,
+                                        (uint32_t)(t * rep.batch + j));
+        row = rows[rep.rows_off + (int)pos];
+      }
+    }
+  }
+  idx[gid] = row;
+  if (j == 0) {
+    cnt[r] = c;
+    adam_t[r] = at;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv1 (recompute) + conv2 (MFMA) + bias + ReLU + 2x2 max-pool.  Block = (half image, slot, model).
+// 9 tiles x 2 channel tiles of 32x32; a tile = 8 pooling windows x 4 pixels, laid out so that the 4
+// pixels of a window are accumulator registers 4g..4g+3 of one lane: the pool is a register max.
+// ------------------------------------------------------------------------------------------------
+constexpr int FWD_THREADS = 192;
+
+__global__ __launch_bounds__(FWD_THREADS) void conv_fwd_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
+    int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, float* __restrict__ pooled,
+    uint8_t* __restrict__ code) {
+  __shared__ float img_s[16 * IMG];
+  __shared__ float w1_s[9 * C1 + C1];
+  __shared__ float a1_s[14 * A1 * A1P];
+  const int half = blockIdx.x;
+  const int j = blockIdx.y;
+  const int r = blockIdx.z;
+  const int count = cnt ? cnt[r] : cnt_all;
+  if (j >= count) return;
+  const int tid = threadIdx.x;
+  const int row = idx ? idx[(int64_t)r * bmax + j] : row_base + j;
+  const float* P = params + (int64_t)r * stride;
+  const float* xi = x + (int64_t)row * (IMG * IMG) + half * 12 * IMG;
+  for (int e = tid; e < 16 * IMG; e += FWD_THREADS) img_s[e] = xi[e];
+  for (int e = tid; e < 9 * C1 + C1; e += FWD_THREADS) w1_s[e] = P[OFF_W1 + e];
+  __syncthreads();
+  // conv1 + ReLU for local rows 0..13 (global 12*half + lr)
+  for (int e = tid; e < 14 * A1 * C1; e += FWD_THREADS) {
+    const int ci = e & 31;
+    const int pos = e >> 5;
+    const int lr = pos / A1, lc = pos % A1;
+    float acc = w1_s[9 * C1 + ci];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) acc += img_s[(lr + ky) * IMG + lc + kx] * w1_s[(ky * 3 + kx) * C1 + ci];
+    a1_s[pos * A1P + ci] = fmaxf(acc, 0.0f);
+  }
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int m = lane & 31;
+  const int kh = lane >> 5;
+  int pbase[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int t = wave + 3 * u;
+    const int wi = 8 * t + (m >> 2);
+    const int pr = wi / PL, pc = wi % PL;
+    const int q = m & 3;
+    const int oy = 2 * pr + (q >> 1), ox = 2 * pc + (q & 1);
+    pbase[u] = (oy * A1 + ox) * A1P;
+  }
+  floatx16 acc[3][2];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
+  const float* W2 = P + OFF_W2;
+  for (int kyx = 0; kyx < 9; ++kyx) {
+    const int ky = kyx / 3, kx = kyx % 3;
+    const int off = (ky * A1 + kx) * A1P;
+    const float* w2k = W2 + (int64_t)kyx * C1 * C2;
+#pragma unroll 8
+    for (int c2 = 0; c2 < 16; ++c2) {
+      const int ci = 2 * c2 + kh;
+      const float b0 = w2k[ci * C2 + m];
+      const float b1 = w2k[ci * C2 + 32 + m];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const float a = a1_s[pbase[u] + off + ci];
+        acc[u][0] = mfma32(a, b0, acc[u][0]);
+        acc[u][1] = mfma32(a, b1, acc[u][1]);
+      }
+    }
+  }
+  // epilogue: bias, ReLU, 2x2 max-pool (first max in window scan order), argmax code
+  float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
+  uint8_t* outc = code ? code + ((int64_t)r * bmax + j) * FEAT : nullptr;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int t = wave + 3 * u;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int co = nt * 32 + m;
+      const float bias = P[OFF_B2 + co];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int wi = 8 * t + 2 * g + kh;
+        const int py = 6 * half + wi / PL, px = wi % PL;
+        float best = acc[u][nt][4 * g] + bias;
+        int arg = 0;
+#pragma unroll
+        for (int qq = 1; qq < 4; ++qq) {
+          const float z = acc[u][nt][4 * g + qq] + bias;
+          if (z > best) { best = z; arg = qq; }
+        }
+        const int pidx = (py * PL + px) * C2 + co;
+        outp[pidx] = fmaxf(best, 0.0f);
+        if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense(128) + ReLU:  H[r][m][n] = relu(sum_k A[r][m][k] W3[r][k][n] + b3[n]).  Block = 32 rows x 128.
+// ------------------------------------------------------------------------------------------------
+constexpr int DF_K = 64;
+
+__global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict__ A, int64_t a_rstride,
+                                                        const int32_t* __restrict__ cnt, int cnt_all, int bmax,
+                                                        const float* __restrict__ params, int64_t stride,
+                                                        float* __restrict__ H) {
+  __shared__ float a_s[32 * (DF_K + 1)];
+  const int r = blockIdx.y;
+  const int m0 = blockIdx.x * 32;
+  const int count = cnt ? cnt[r] : cnt_all;
+  if (m0 >= count) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n0 = wave * 32;
+  const int kh = lane >> 5;
+  const float* Ar = A + (int64_t)r * a_rstride;
+  const float* W = params + (int64_t)r * stride + OFF_W3;
+  floatx16 acc = zero16();
+  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
+    // stage A[m0..m0+31][k0..k0+63] (rows beyond count are zero)
+    for (int e = tid; e < 32 * DF_K; e += 256) {
+      const int mm = e / DF_K, kk = e % DF_K;
+      a_s[mm * (DF_K + 1) + kk] = (m0 + mm < count) ? Ar[(int64_t)(m0 + mm) * FEAT + k0 + kk] : 0.0f;
+    }
+    __syncthreads();
+    const float* Wk = W + (int64_t)k0 * HID + n0 + (lane & 31);
+#pragma unroll 8
+    for (int s = 0; s < DF_K / 2; ++s) {
+      const float a = a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh];
+      const float b = Wk[(int64_t)(2 * s + kh) * HID];
+      acc = mfma32(a, b, acc);
+    }
+    __syncthreads();
+  }
+  const float bias = params[(int64_t)r * stride + OFF_B3 + n0 + (lane & 31)];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+    if (m0 + row < count)
+      H[((int64_t)r * bmax + m0 + row) * HID + n0 + (lane & 31)] = fmaxf(acc[reg] + bias, 0.0f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Keras 2.3.1 Adam (fresh state when t == 1: FedAvg builds a new optimizer per partner fit)
+// ------------------------------------------------------------------------------------------------
+struct AdamCfg {
+  float lr_t, b1, b2, eps;
+  bool reset;
+};
+
+__device__ __forceinline__ AdamCfg adam_cfg(int t, float lr, float b1, float b2, float eps) {
+  AdamCfg c;
+  const float tf = (float)t;
+  c.lr_t = lr * (sqrtf(1.0f - powf(b2, tf)) / (1.0f - powf(b1, tf)));
+  c.b1 = b1;
+  c.b2 = b2;
+  c.eps = eps;
+  c.reset = (t == 1);
+  return c;
+}
+
+__device__ __forceinline__ void adam_apply(float& p, float& m, float& v, float g, const AdamCfg& c) {
+  const float m0 = c.reset ? 0.0f : m;
+  const float v0 = c.reset ? 0.0f : v;
+  const float mt = c.b1 * m0 + (1.0f - c.b1) * g;
+  const float vt = c.b2 * v0 + (1.0f - c.b2) * (g * g);
+  p = p - c.lr_t * mt / (sqrtf(vt) + c.eps);
+  m = mt;
+  v = vt;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Head: Dense(10) + softmax-CE gradient (mean over the batch), dW4/db4 + Adam, dh = dlogits W4^T * relu'
+// One block per replica.
+// ------------------------------------------------------------------------------------------------
+constexpr int HEAD_CHUNK = 256;
+
+__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, const int32_t* __restrict__ idx,
+                                                   const int32_t* __restrict__ labels, const int32_t* __restrict__ cnt,
+                                                   const int32_t* __restrict__ adam_t, int bmax,
+                                                   float* __restrict__ params, float* __restrict__ adam_m,
+                                                   float* __restrict__ adam_v, int64_t stride,
+                                                   float* __restrict__ dH, float lr, float b1, float b2, float eps) {
+  __shared__ float w4_s[HID * NCLS + NCLS];
+  __shared__ float dl_s[HEAD_CHUNK * NCLS];
+  const int r = blockIdx.x;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  float* P = params + (int64_t)r * stride;
+  for (int e = tid; e < HID * NCLS + NCLS; e += 256) w4_s[e] = P[OFF_W4 + e];
+  __syncthreads();
+  const float inv_b = 1.0f / (float)count;
+  float gacc[6] = {0, 0, 0, 0, 0, 0};  // dW4 elements tid, tid+256, ... (1290 = W4 + b4)
+  const float* Hr = H + (int64_t)r * bmax * HID;
+  for (int c0 = 0; c0 < count; c0 += HEAD_CHUNK) {
+    const int cn = min(HEAD_CHUNK, count - c0);
+    if (tid < cn) {
+      const int jj = c0 + tid;
+      const float* h = Hr + (int64_t)jj * HID;
+      float z[NCLS];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) z[o] = w4_s[HID * NCLS + o];
+      for (int c = 0; c < HID; ++c) {
+        const float hv = h[c];
+#pragma unroll
+        for (int o = 0; o < NCLS; ++o) z[o] += hv * w4_s[c * NCLS + o];
+      }
+      float mx = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o) mx = fmaxf(mx, z[o]);
+      float s = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) { z[o] = expf(z[o] - mx); s += z[o]; }
+      const int y = labels[idx[(int64_t)r * bmax + jj]];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) dl_s[tid * NCLS + o] = (z[o] / s - (o == y ? 1.0f : 0.0f)) * inv_b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + 256 * u;
+      if (e < HID * NCLS) {
+        const int c = e / NCLS, o = e % NCLS;
+        float a = 0.0f;
+        for (int jj = 0; jj < cn; ++jj) a += Hr[(int64_t)(c0 + jj) * HID + c] * dl_s[jj * NCLS + o];
+        gacc[u] += a;
+      } else if (e < HID * NCLS + NCLS) {
+        const int o = e - HID * NCLS;
+        float a = 0.0f;
+        for (int jj = 0; jj < cn; ++jj) a += dl_s[jj * NCLS + o];
+        gacc[u] += a;
+      }
+    }
+    for (int e = tid; e < cn * HID; e += 256) {
+      const int jj = e / HID, c = e % HID;
+      const float hv = Hr[(int64_t)(c0 + jj) * HID + c];
+      float a = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) a += dl_s[jj * NCLS + o] * w4_s[c * NCLS + o];
+      dH[((int64_t)r * bmax + c0 + jj) * HID + c] = hv > 0.0f ? a : 0.0f;
+    }
+    __syncthreads();
+  }
+  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
+  float* Mr = adam_m + (int64_t)r * stride;
+  float* Vr = adam_v + (int64_t)r * stride;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const int e = tid + 256 * u;
+    if (e < HID * NCLS + NCLS) {
+      const int64_t o = OFF_W4 + e;  // W4 and b4 are contiguous
+      float p = P[o], mm = Mr[o], vv = Vr[o];
+      adam_apply(p, mm, vv, gacc[u], cfg);
+      P[o] = p;
+      Mr[o] = mm;
+      Vr[o] = vv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense(128) backward + Adam, per 64-row slice of W3 (block = 256 threads: row = tid/4, 32 cols each)
+// dp[j][k] = sum_c dh[j][c] W3[k][c];  dW3[k][c] = sum_j p[j][k] dh[j][c];  db3 (slice 0 block)
+// ------------------------------------------------------------------------------------------------
+constexpr int D1_ROWS = 64;
+constexpr int D1_SCHUNK = 32;
+
+__global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
+    const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
+    const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
+    float* __restrict__ adam_v, int64_t stride, float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
+  __shared__ float dh_s[D1_SCHUNK * HID];
+  __shared__ float p_s[D1_SCHUNK * D1_ROWS];
+  const int r = blockIdx.y;
+  const int k0 = blockIdx.x * D1_ROWS;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  const int rowl = tid >> 2;
+  const int cq = (tid & 3) * 32;
+  float* W = params + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
+  float w[32], g[32];
+#pragma unroll
+  for (int i = 0; i < 32; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(W + i);
+    w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
+    g[i] = g[i + 1] = g[i + 2] = g[i + 3] = 0.0f;
+  }
+  const float* Pr = Pool + (int64_t)r * bmax * FEAT;
+  const float* dHr = dH + (int64_t)r * bmax * HID;
+  float* dPr = dPool + (int64_t)r * bmax * FEAT;
+  for (int c0 = 0; c0 < count; c0 += D1_SCHUNK) {
+    const int cn = min(D1_SCHUNK, count - c0);
+    for (int e = tid; e < cn * HID; e += 256) dh_s[e] = dHr[(int64_t)c0 * HID + e];
+    for (int e = tid; e < cn * D1_ROWS; e += 256) {
+      const int jj = e / D1_ROWS, kk = e % D1_ROWS;
+      p_s[e] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + kk];
+    }
+    __syncthreads();
+    for (int jj = 0; jj < cn; ++jj) {
+      const float pv = p_s[jj * D1_ROWS + rowl];
+      float d = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const float dh = dh_s[jj * HID + cq + i];
+        g[i] += pv * dh;
+        d += dh * w[i];
+      }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      if ((tid & 3) == 0) dPr[(int64_t)(c0 + jj) * FEAT + k0 + rowl] = d;
+    }
+    __syncthreads();
+  }
+  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
+  float* Mr = adam_m + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
+  float* Vr = adam_v + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
+#pragma unroll
+  for (int i = 0; i < 32; i += 4) {
+    float4 mv = *reinterpret_cast<const float4*>(Mr + i);
+    float4 vv = *reinterpret_cast<const float4*>(Vr + i);
+    float pw[4] = {w[i], w[i + 1], w[i + 2], w[i + 3]};
+    float pm[4] = {mv.x, mv.y, mv.z, mv.w};
+    float pv[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) adam_apply(pw[q], pm[q], pv[q], g[i + q], cfg);
+    *reinterpret_cast<float4*>(W + i) = make_float4(pw[0], pw[1], pw[2], pw[3]);
+    *reinterpret_cast<float4*>(Mr + i) = make_float4(pm[0], pm[1], pm[2], pm[3]);
+    *reinterpret_cast<float4*>(Vr + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  }
+  if (blockIdx.x == 0 && tid < HID) {
+    float gb = 0.0f;
+    for (int jj = 0; jj < count; ++jj) gb += dHr[(int64_t)jj * HID + tid];
+    const int64_t o = (int64_t)r * stride + OFF_B3 + tid;
+    adam_apply(params[o], adam_m[o], adam_v[o], gb, cfg);
+  }
+}
+
+// W2 [kyx][ci][co] -> W2t [kyx][co][ci]
+__global__ void transpose_w2_kernel(const float* __restrict__ params, int64_t stride, const int32_t* __restrict__ cnt,
+                                    float* __restrict__ w2t) {
+  const int r = blockIdx.y;
+  if (cnt && cnt[r] == 0) return;
+  const float* W2 = params + (int64_t)r * stride + OFF_W2;
+  float* T = w2t + (int64_t)r * (9 * C1 * C2);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 9 * C1 * C2; e += gridDim.x * blockDim.x) {
+    const int kyx = e / (C1 * C2);
+    const int rem = e % (C1 * C2);
+    const int co = rem / C1, ci = rem % C1;
+    T[e] = W2[(kyx * C1 + ci) * C2 + co];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv2 data gradient + conv1 backward.  Block = one sample (4 waves, 22 row tiles of 32 positions).
+// dZ2[oy][ox][co] = dp[py][px][co] if the window's argmax is (oy,ox) and its max was > 0, else 0.
+// ------------------------------------------------------------------------------------------------
+constexpr int BWD_THREADS = 256;
+
+__global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
+    const float* __restrict__ params, int64_t stride, const float* __restrict__ w2t,
+    const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
+  __shared__ float dz_s[PL * PL * C2];
+  __shared__ uint8_t sel_s[PL * PL * C2];
+  __shared__ float img_s[IMG * IMG];
+  __shared__ float w1_s[9 * C1 + C1];
+  __shared__ float red_s[4][10 * 32];
+  const int j = blockIdx.x;
+  const int r = blockIdx.y;
+  if (j >= cnt[r]) return;
+  const int tid = threadIdx.x;
+  const int row = idx[(int64_t)r * bmax + j];
+  const float* P = params + (int64_t)r * stride;
+  const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
+  const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
+  for (int e = tid; e < FEAT; e += BWD_THREADS) {
+    const uint8_t c = cd[e];
+    const bool pos = (c & 0x80) != 0;
+    dz_s[e] = pos ? dp[e] : 0.0f;
+    sel_s[e] = pos ? (c & 3) : 4;
+  }
+  for (int e = tid; e < IMG * IMG; e += BWD_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + e];
+  for (int e = tid; e < 9 * C1 + C1; e += BWD_THREADS) w1_s[e] = P[OFF_W1 + e];
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31;
+  const int kh = lane >> 5;
+  const float* T = w2t + (int64_t)r * (9 * C1 * C2);
+  float gw1[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) gw1[i] = 0.0f;
+  float gb1 = 0.0f;
+  // tiles t = wave, wave+4, ...  (22 tiles of 32 positions over 676)
+  for (int t = wave; t < 22; t += 4) {
+    const int mpos = t * 32 + n;  // A row of this lane
+    const int iy = mpos / A1, ix = mpos % A1;
+    floatx16 acc = zero16();
+    for (int kyx = 0; kyx < 9; ++kyx) {
+      const int ky = kyx / 3, kx = kyx % 3;
+      const int oy = iy - ky, ox = ix - kx;
+      const bool inb = (mpos < A1 * A1) && oy >= 0 && oy < Z2 && ox >= 0 && ox < Z2;
+      const int cell = inb ? ((oy >> 1) * PL + (ox >> 1)) * C2 : 0;
+      const int q = inb ? ((oy & 1) * 2 + (ox & 1)) : 5;
+      const float* Tk = T + kyx * C2 * C1 + n;
+#pragma unroll 8
+      for (int c2 = 0; c2 < 32; ++c2) {
+        const int co = 2 * c2 + kh;
+        const float a = (sel_s[cell + co] == q) ? dz_s[cell + co] : 0.0f;
+        const float b = Tk[co * C1];
+        acc = mfma32(a, b, acc);
+      }
+    }
+    // epilogue: ReLU' of recomputed conv1 output, conv1 weight gradient
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int prow = t * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+      if (prow < A1 * A1) {
+        const int py = prow / A1, px = prow % A1;
+        const int ci = n;
+        float a1 = w1_s[9 * C1 + ci];
+        float pix[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          pix[k] = img_s[(py + k / 3) * IMG + px + k % 3];
+          a1 += pix[k] * w1_s[k * C1 + ci];
+        }
+        if (a1 > 0.0f) {
+          const float dz = acc[reg];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) gw1[k] += pix[k] * dz;
+          gb1 += dz;
+        }
+      }
+    }
+  }
+  // reduce over lane halves (same ci) and waves
+#pragma unroll
+  for (int k = 0; k < 9; ++k) gw1[k] += __shfl_xor(gw1[k], 32, 64);
+  gb1 += __shfl_xor(gb1, 32, 64);
+  if (kh == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) red_s[wave][k * 32 + n] = gw1[k];
+    red_s[wave][9 * 32 + n] = gb1;
+  }
+  __syncthreads();
+  float* out = w1_part + ((int64_t)r * bmax + j) * MPLC_CNN_W1P;
+  for (int e = tid; e < 10 * 32; e += BWD_THREADS)
+    out[e] = (red_s[0][e] + red_s[1][e]) + (red_s[2][e] + red_s[3][e]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv2 weight gradient: dW2[kyx*32+ci][co] = sum_px a1[py+ky][px+kx][ci] dZ2[px][co]; db2.
+// Block = (split s, replica r): samples [8s, 8s+8); 3 waves x (3 row tiles x 2 col tiles).
+// Output rows of 4 conv2 pixels-rows at a time (a band): conv1 rows recomputed into LDS per band.
+// ------------------------------------------------------------------------------------------------
+constexpr int WG_THREADS = 192;
+constexpr int WG_SAMPLES = 8;  // samples per wgrad split (fixed: reproducible sums)
+
+__global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
+    const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
+    int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
+    const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
+  __shared__ float img_s[IMG * IMG];
+  __shared__ float w1_s[9 * C1 + C1];
+  __shared__ float a1_s[6 * A1 * C1];
+  __shared__ float dz_s[2 * PL * C2];
+  __shared__ uint8_t sel_s[2 * PL * C2];
+  __shared__ float red_s[3][2][32];
+  const int sp = blockIdx.x;
+  const int r = blockIdx.y;
+  const int count = cnt[r];
+  // samples [sp*WG_SAMPLES, (sp+1)*WG_SAMPLES): the split of a replica depends only on its own batch,
+  // so its summation order (and v(S)) does not depend on which other replicas share the launch
+  const int j_begin = sp * WG_SAMPLES;
+  const int j_end = min(count, j_begin + WG_SAMPLES);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 31;
+  const int kh = lane >> 5;
+  const float* P = params + (int64_t)r * stride;
+  for (int e = tid; e < 9 * C1 + C1; e += WG_THREADS) w1_s[e] = P[OFF_W1 + e];
+  floatx16 acc[3][2];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
+  float gb[2] = {0.0f, 0.0f};
+  for (int j = j_begin; j < j_end; ++j) {
+    const int row = idx[(int64_t)r * bmax + j];
+    const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
+    const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
+    __syncthreads();
+    for (int e = tid; e < IMG * IMG; e += WG_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + e];
+    for (int band = 0; band < 6; ++band) {
+      __syncthreads();
+      // conv1 rows 4*band .. 4*band+5 and pooled rows 2*band, 2*band+1
+      for (int e = tid; e < 6 * A1 * C1; e += WG_THREADS) {
+        const int ci = e & 31;
+        const int pos = e >> 5;
+        const int lr = pos / A1, lc = pos % A1;
+        const int gy = 4 * band + lr;
+        float a = w1_s[9 * C1 + ci];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a += img_s[(gy + k / 3) * IMG + lc + k % 3] * w1_s[k * C1 + ci];
+        a1_s[e] = fmaxf(a, 0.0f);
+      }
+      for (int e = tid; e < 2 * PL * C2; e += WG_THREADS) {
+        const int ge = band * 2 * PL * C2 + e;
+        const uint8_t c = cd[ge];
+        const bool pos = (c & 0x80) != 0;
+        dz_s[e] = pos ? dp[ge] : 0.0f;
+        sel_s[e] = pos ? (c & 3) : 4;
+      }
+      __syncthreads();
+      // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh)
+#pragma unroll 4
+      for (int s = 0; s < 48; ++s) {
+        const int px = 2 * s + kh;          // 0..95 within band
+        const int oyl = px / Z2, ox = px % Z2;  // oyl 0..3
+        const int cell = ((oyl >> 1) * PL + (ox >> 1)) * C2;
+        const int q = (oyl & 1) * 2 + (ox & 1);
+        const float bz0 = (sel_s[cell + m] == q) ? dz_s[cell + m] : 0.0f;
+        const float bz1 = (sel_s[cell + 32 + m] == q) ? dz_s[cell + 32 + m] : 0.0f;
+        if (wave == 0) { gb[0] += bz0; gb[1] += bz1; }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int kyx = 3 * wave + u;     // row tile = 32 consecutive (kyx, ci)
+          const int ky = kyx / 3, kx = kyx % 3;
+          const float a = a1_s[((oyl + ky) * A1 + ox + kx) * C1 + m];
+          acc[u][0] = mfma32(a, bz0, acc[u][0]);
+          acc[u][1] = mfma32(a, bz1, acc[u][1]);
+        }
+      }
+    }
+  }
+  float* out = w2_part + ((int64_t)r * splits + sp) * MPLC_CNN_W2P;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int kyx = 3 * wave + u;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int ci = (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+        out[(kyx * C1 + ci) * C2 + nt * 32 + m] = acc[u][nt][reg];
+      }
+    }
+  }
+  if (wave == 0) {
+    gb[0] += __shfl_xor(gb[0], 32, 64);
+    gb[1] += __shfl_xor(gb[1], 32, 64);
+    if (kh == 0) {
+      out[9 * C1 * C2 + m] = gb[0];
+      out[9 * C1 * C2 + 32 + m] = gb[1];
+    }
+  }
+}
+
+// Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
+__global__ void adam_small_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ adam_t, int bmax,
+                                  int splits, const float* __restrict__ w1_part, const float* __restrict__ w2_part,
+                                  float* __restrict__ params, float* __restrict__ adam_m, float* __restrict__ adam_v,
+                                  int64_t stride, float lr, float b1, float b2, float eps) {
+  const int r = blockIdx.y;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= OFF_W3) return;
+  float g = 0.0f;
+  if (e < OFF_W2) {
+    const float* w = w1_part + (int64_t)r * bmax * MPLC_CNN_W1P + e;
+    for (int jj = 0; jj < count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];
+  } else {
+    const float* w = w2_part + (int64_t)r * splits * MPLC_CNN_W2P + (e - OFF_W2);
+    const int used = (count + WG_SAMPLES - 1) / WG_SAMPLES;
+    for (int s = 0; s < used; ++s) g += w[(int64_t)s * MPLC_CNN_W2P];
+  }
+  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
+  const int64_t o = (int64_t)r * stride + e;
+  adam_apply(params[o], adam_m[o], adam_v[o], g, cfg);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Evaluation head: logits, accuracy count and summed cross-entropy per model (deterministic order).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict__ H, int count, int chunk,
+                                                        const int32_t* __restrict__ labels, int row_base,
+                                                        const float* __restrict__ params, int64_t stride,
+                                                        int32_t* __restrict__ correct, double* __restrict__ loss_sum) {
+  __shared__ float w4_s[HID * NCLS + NCLS];
+  __shared__ double ls[256];
+  __shared__ int cs[256];
+  const int mdl = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* P = params + (int64_t)mdl * stride;
+  for (int e = tid; e < HID * NCLS + NCLS; e += 256) w4_s[e] = P[OFF_W4 + e];
+  __syncthreads();
+  double lsum = 0.0;
+  int csum = 0;
+  for (int jj = tid; jj < count; jj += 256) {
+    const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
+    float z[NCLS];
+#pragma unroll
+    for (int o = 0; o < NCLS; ++o) z[o] = w4_s[HID * NCLS + o];
+    for (int c = 0; c < HID; ++c) {
+      const float hv = h[c];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) z[o] += hv * w4_s[c * NCLS + o];
+    }
+    int am = 0;
+    float mx = z[0];
+#pragma unroll
+    for (int o = 1; o < NCLS; ++o)
+      if (z[o] > mx) { mx = z[o]; am = o; }
+    float s = 0.0f;
+#pragma unroll
+    for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
+    const int y = labels[row_base + jj];
+    lsum += (double)(logf(s) + mx - z[y]);
+    csum += (am == y) ? 1 : 0;
+  }
+  ls[tid] = lsum;
+  cs[tid] = csum;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if (tid < off) { ls[tid] += ls[tid + off]; cs[tid] += cs[tid + off]; }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    correct[mdl] += cs[0];
+    loss_sum[mdl] += ls[0];
+  }
+}
+
+inline int launch_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MPLC_OK : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mplc_cnn_stride(void) { return MPLC_CNN_STRIDE; }
+
+int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
+  if (!params || !keys || n_models < 1 || n_models > 65535 || stride < MPLC_CNN_NPARAM) return MPLC_E_ARG;
+  init_params_kernel<<<dim3(512, n_models), 256, 0, (hipStream_t)stream>>>(params, stride, keys);
+  return launch_status();
+}
+
+int mplc_cnn_copy_rows(float* dst, const float* src, int64_t stride, const int32_t* map, int n_rows, void* stream) {
+  if (!dst || !src || !map || n_rows < 1 || n_rows > 65535 || (stride & 3)) return MPLC_E_ARG;
+  copy_rows_kernel<<<dim3(256, n_rows), 256, 0, (hipStream_t)stream>>>(dst, src, stride, map);
+  return launch_status();
+}
+
+int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
+  if (!t || t->n_rep < 1 || t->n_rep > 65535 || t->bmax < 1) return MPLC_E_ARG;
+  if (t->w2_splits != (t->bmax + WG_SAMPLES - 1) / WG_SAMPLES) return MPLC_E_SHAPE;
+  if (!t->reps || !t->rows || !t->splits || !t->x || !t->labels || !t->params || !t->adam_m || !t->adam_v ||
+      !t->idx || !t->cnt || !t->adam_t || !t->pooled || !t->code || !t->hidden || !t->dhidden || !t->dpooled ||
+      !t->w1_part || !t->w2_part || !t->w2t)
+    return MPLC_E_ARG;
+  if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int R = t->n_rep, B = t->bmax;
+  const int64_t S = MPLC_CNN_STRIDE;
+  const int64_t slots = (int64_t)R * B;
+  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->step,
+                                                                   t->minibatch_count, t->round_len, t->epochs,
+                                                                   t->idx, t->cnt, t->adam_t);
+  conv_fwd_kernel<<<dim3(2, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->pooled,
+                                                         t->code);
+  dense_fwd_kernel<<<dim3((B + 31) / 32, R), 256, 0, s>>>(t->pooled, (int64_t)B * FEAT, t->cnt, 0, B, t->params, S,
+                                                          t->hidden);
+  head_kernel<<<R, 256, 0, s>>>(t->hidden, t->idx, t->labels, t->cnt, t->adam_t, B, t->params, t->adam_m, t->adam_v,
+                                S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps);
+  dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+                                                                  t->params, t->adam_m, t->adam_v, S, t->dpooled,
+                                                                  t->lr, t->beta1, t->beta2, t->eps);
+  transpose_w2_kernel<<<dim3(18, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
+  conv_bwd_data_kernel<<<dim3(B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
+                                                          t->code, t->w1_part);
+  conv_wgrad_kernel<<<dim3(t->w2_splits, R), WG_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->w2_splits, t->params,
+                                                                 S, t->dpooled, t->code, t->w2_part);
+  adam_small_kernel<<<dim3((OFF_W3 + 255) / 256, R), 256, 0, s>>>(t->cnt, t->adam_t, B, t->w2_splits, t->w1_part,
+                                                                 t->w2_part, t->params, t->adam_m, t->adam_v, S,
+                                                                 t->lr, t->beta1, t->beta2, t->eps);
+  return launch_status();
+}
+
+int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
+                      int n_samples, int chunk, float* pooled, float* hidden, int32_t* correct, double* loss_sum,
+                      void* stream) {
+  if (!params || !x || !labels || !pooled || !hidden || !correct || !loss_sum) return MPLC_E_ARG;
+  if (n_models < 1 || n_models > 65535 || n_samples < 1 || chunk < 1 || chunk > 65535 || stride != MPLC_CNN_STRIDE)
+    return MPLC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  for (int s0 = 0; s0 < n_samples; s0 += chunk) {
+    const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
+    conv_fwd_kernel<<<dim3(2, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
+                                                                  pooled, nullptr);
+    dense_fwd_kernel<<<dim3((cn + 31) / 32, n_models), 256, 0, s>>>(pooled, (int64_t)chunk * FEAT, nullptr, cn, chunk,
+                                                                    params, stride, hidden);
+    eval_head_kernel<<<n_models, 256, 0, s>>>(hidden, cn, chunk, labels, s0, params, stride, correct, loss_sum);
+    const int st = launch_status();
+    if (st) return st;
+  }
+  return MPLC_OK;
+}
+
+}  // extern "C"

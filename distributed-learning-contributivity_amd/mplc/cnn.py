@@ -1,0 +1,333 @@
+"""Host driver of the batched MNIST CNN trainer (csrc/mnist_cnn.hip, include/mplc_hip_cnn.h).
+
+Trains a batch of coalitions at once and returns their test accuracies.  Semantics follow the
+reference's learning path for the MNIST model (mplc/dataset.py:457-479):
+  FedAvg coalition (|S| >= 2), mplc/multi_partner_learning.py:195-216, 285-334:
+    init random model; per epoch, each partner's rows are permuted and split into M minibatches
+    (mplc/partner.py:155-167); per round m every partner starts from the global model with a FRESH Adam
+    and runs ceil(L_m / bs_p) steps of bs_p samples (Keras fit, 1 epoch, shuffled); the round ends with
+    the data-volume (or uniform) weighted average (mplc/mpl_utils.py:90-115) -> next global model.
+    Early stopping (when enabled and E > PATIENCE): val loss of the global model at the start of epoch e
+    compared with epoch e - 10 (mplc/multi_partner_learning.py:177-193).
+  Singleton (|S| == 1), mplc/multi_partner_learning.py:238-269: one Keras fit over all rows, E epochs,
+    batch bs_p, persistent Adam, Keras EarlyStopping(val_loss, patience=10).
+  v(S) = test accuracy of the final model (mplc/multi_partner_learning.py:158-169).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from .fedavg import aggregation_weights
+
+STRIDE = 1199936
+NPARAM = 1199882
+FEAT = 9216
+HID = 128
+W1P = 320
+W2P = 18496
+WG_SAMPLES = 8
+PATIENCE = 10
+
+REP_IDLE, REP_FEDAVG, REP_SINGLE = -1, 0, 1
+M64 = (1 << 64) - 1
+
+
+class ReplicaT(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_rows", ctypes.c_int32), ("batch", ctypes.c_int32),
+                ("rows_off", ctypes.c_int32), ("split_off", ctypes.c_int32), ("model", ctypes.c_int32),
+                ("key", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(ReplicaT) == 32
+
+REPLICA_DTYPE = np.dtype([("kind", np.int32), ("n_rows", np.int32), ("batch", np.int32), ("rows_off", np.int32),
+                          ("split_off", np.int32), ("model", np.int32), ("key", np.uint64)])
+assert REPLICA_DTYPE.itemsize == 32
+
+
+class TrainT(ctypes.Structure):
+    _fields_ = [("n_rep", ctypes.c_int32), ("bmax", ctypes.c_int32), ("w2_splits", ctypes.c_int32),
+                ("pad0", ctypes.c_int32), ("step", ctypes.c_int32), ("minibatch_count", ctypes.c_int32),
+                ("round_len", ctypes.c_int32), ("epochs", ctypes.c_int32),
+                ("reps", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("splits", ctypes.c_void_p),
+                ("x", ctypes.c_void_p), ("labels", ctypes.c_void_p),
+                ("params", ctypes.c_void_p), ("adam_m", ctypes.c_void_p), ("adam_v", ctypes.c_void_p),
+                ("idx", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("adam_t", ctypes.c_void_p),
+                ("pooled", ctypes.c_void_p), ("code", ctypes.c_void_p), ("hidden", ctypes.c_void_p),
+                ("dhidden", ctypes.c_void_p), ("dpooled", ctypes.c_void_p), ("w1_part", ctypes.c_void_p),
+                ("w2_part", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
+                ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("eps", ctypes.c_float)]
+
+
+_BOUND = False
+
+
+def _bind():
+    global _BOUND
+    if _BOUND:
+        return
+    c_int, c_int64, vp = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
+    _native.register("mplc_cnn_stride", c_int, [])
+    _native.register("mplc_cnn_init_params", c_int, [vp, c_int64, vp, c_int, vp])
+    _native.register("mplc_cnn_copy_rows", c_int, [vp, vp, c_int64, vp, c_int, vp])
+    _native.register("mplc_cnn_train_step", c_int, [ctypes.POINTER(TrainT), vp])
+    _native.register("mplc_cnn_evaluate", c_int, [vp, c_int64, c_int, vp, vp, c_int, c_int, vp, vp, vp, vp, vp])
+    lib = _native.lib()
+    if lib.mplc_cnn_stride() != STRIDE:
+        raise RuntimeError("libmplc_hip.so CNN layout mismatch; rebuild")
+    _BOUND = True
+
+
+# ------------------------------------------------------------------------------------------------
+# keys (restated bit for bit in oracle/cnn.py)
+# ------------------------------------------------------------------------------------------------
+def mix64(z):
+    z &= M64
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & M64
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & M64
+    return z ^ (z >> 31)
+
+
+def init_key(seed, mask):
+    return mix64(mix64((seed + 0x1517) & M64) ^ mask)
+
+
+def shuffle_key(seed, mask, partner):
+    return mix64(mix64(mix64((seed + 0x5EED) & M64) ^ mask) ^ (partner + 1))
+
+
+def minibatch_bounds(n, M):
+    """[0, int(1/M*n), ..., int((M-1)/M*n), n] exactly as np.split's indices in mplc/partner.py:159-167."""
+    split_indices = np.arange(1, M + 1) / M
+    inner = (split_indices[:-1] * n).astype(int)
+    return [0] + [int(v) for v in inner] + [int(n)]
+
+
+class TrainBatch:
+    """Device state of one lockstep batch: coalition global rows, replica rows, Adam state, workspaces."""
+
+    def __init__(self, eng, coalitions, epochs, lib):
+        import torch
+        self.eng, self.lib = eng, lib
+        self.coalitions = coalitions
+        self.epochs = epochs
+        dev = eng.device
+        self.dev = dev
+        self.stream = _native.stream_handle(dev)
+        C = len(coalitions)
+        sizes = eng.partner_sizes
+        reps, src, first, single = [], [], [], []
+        for ci, coal in enumerate(coalitions):
+            mask = sum(1 << p for p in coal)
+            first.append(len(reps))
+            single.append(len(coal) == 1)
+            for p in coal:
+                reps.append((REP_SINGLE if len(coal) == 1 else REP_FEDAVG, sizes[p], eng.batch_sizes[p],
+                             eng.rows_off[p], eng.split_off[p], len(reps), shuffle_key(eng.seed, mask, p)))
+                src.append(ci)
+        first.append(len(reps))
+        self.coal_first, self.coal_is_single = first, single
+        R = len(reps)
+        self.R, self.C = R, C
+        self.rep_arr = np.zeros(R, dtype=REPLICA_DTYPE)
+        for i, rp in enumerate(reps):
+            self.rep_arr[i] = rp
+        self.bmax = int(max(eng.batch_sizes[p] for coal in coalitions for p in coal))
+        M = eng.minibatch_count
+        round_len, single_steps = 1, 0
+        for coal in coalitions:
+            for p in coal:
+                if len(coal) > 1:
+                    b = eng.bounds[p]
+                    for m in range(M):
+                        round_len = max(round_len, -(-(b[m + 1] - b[m]) // eng.batch_sizes[p]))
+                else:
+                    single_steps = max(single_steps, epochs * -(-sizes[p] // eng.batch_sizes[p]))
+        self.round_len = round_len
+        self.fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
+        self.total_steps = max(self.fed_steps, single_steps)
+        splits = (self.bmax + WG_SAMPLES - 1) // WG_SAMPLES
+        f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.f32, self.i32 = f32, i32
+        self.glob = torch.empty((C, STRIDE), **f32)
+        self.params = torch.empty((R, STRIDE), **f32)
+        self.adam_m = torch.zeros((R, STRIDE), **f32)
+        self.adam_v = torch.zeros((R, STRIDE), **f32)
+        keys = torch.from_numpy(np.array([init_key(eng.seed, sum(1 << p for p in c)) for c in coalitions],
+                                         dtype=np.uint64).view(np.int64)).to(dev)
+        _native.check(lib.mplc_cnn_init_params(_native.ptr(self.glob), STRIDE, _native.ptr(keys), C, self.stream),
+                      "mplc_cnn_init_params")
+        src_map = torch.tensor(src, **i32)
+        _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), STRIDE,
+                                             _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
+        self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
+        B = self.bmax
+        self.ws = dict(
+            idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
+            pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
+            hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
+            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, W1P), **f32),
+            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, 9 * 64 * 32), **f32))
+        t = TrainT()
+        t.n_rep, t.bmax, t.w2_splits = R, B, splits
+        t.minibatch_count, t.round_len, t.epochs = M, round_len, epochs
+        t.reps, t.rows, t.splits = self.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
+        t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
+        t.params, t.adam_m, t.adam_v = self.params.data_ptr(), self.adam_m.data_ptr(), self.adam_v.data_ptr()
+        for k, v in self.ws.items():
+            setattr(t, k, v.data_ptr())
+        t.lr, t.beta1, t.beta2, t.eps = 0.001, 0.9, 0.999, 1e-7
+        self.t = t
+        self.stopped = np.zeros(C, dtype=bool)
+        self.kind_host = self.rep_arr["kind"].copy()
+        self.run_args = self.make_runs()
+
+    def make_runs(self):
+        """FedAvg aggregation launches: one per contiguous run of live FedAvg coalitions (a coalition's replica
+        rows are contiguous; singletons and stopped coalitions break runs)."""
+        import torch
+        runs, cur = [], []
+        for ci in range(self.C):
+            if self.coal_is_single[ci] or self.stopped[ci]:
+                if cur:
+                    runs.append(cur)
+                cur = []
+            else:
+                cur.append(ci)
+        if cur:
+            runs.append(cur)
+        sizes, first = self.eng.partner_sizes, self.coal_first
+        args = []
+        for run in runs:
+            f = torch.tensor([first[ci] - first[run[0]] for ci in run] + [first[run[-1] + 1] - first[run[0]]],
+                             **self.i32)
+            w, sc = [], []
+            for ci in run:
+                ww, scl = aggregation_weights([sizes[p] for p in self.coalitions[ci]], self.eng.aggregation)
+                w.extend(ww)
+                sc.append(scl)
+            args.append((first[run[0]], run[0], len(run), f, torch.tensor(w, dtype=torch.float64, device=self.dev),
+                         torch.tensor(sc, dtype=torch.float64, device=self.dev)))
+        return args
+
+    def step(self, s):
+        self.t.step = s
+        _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(self.t), self.stream), "mplc_cnn_train_step")
+
+    def aggregate(self):
+        for (r0, c0, nc, first, w, sc) in self.run_args:
+            _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(self.params[r0:]), STRIDE, _native.ptr(first),
+                                                         _native.ptr(w), _native.ptr(sc), nc, NPARAM,
+                                                         _native.ptr(self.glob[c0:c0 + nc]), STRIDE, 1, self.stream),
+                          "mplc_fedavg_aggregate")
+
+    def stop(self, ci):
+        import torch
+        self.stopped[ci] = True
+        self.kind_host[self.coal_first[ci]:self.coal_first[ci + 1]] = REP_IDLE
+        ra = self.rep_arr.copy()
+        ra["kind"] = self.kind_host
+        self.rep_t.copy_(torch.from_numpy(ra.view(np.uint8).copy()).to(self.dev))
+        self.run_args = self.make_runs()
+
+    def finalize(self):
+        """Singleton final models -> their coalition rows; free training state."""
+        import torch
+        single = [ci for ci in range(self.C) if self.coal_is_single[ci]]
+        if single:
+            m = torch.tensor([self.coal_first[ci] for ci in single], **self.i32)
+            tmp = torch.empty((len(single), STRIDE), **self.f32)
+            _native.check(self.lib.mplc_cnn_copy_rows(_native.ptr(tmp), _native.ptr(self.params), STRIDE,
+                                                      _native.ptr(m), len(single), self.stream), "mplc_cnn_copy_rows")
+            self.glob[torch.tensor(single, device=self.dev)] = tmp
+        self.params = self.adam_m = self.adam_v = None
+        self.ws = None
+        return self.glob
+
+
+class CnnBatchTrainer:
+    """Trains one batch of coalitions (all on the current HIP device) and evaluates them."""
+
+    def __init__(self, engine):
+        _bind()
+        self.eng = engine
+        self.lib = _native.lib()
+
+    def prepare(self, coalitions, epochs):
+        return TrainBatch(self.eng, coalitions, epochs, self.lib)
+
+    def run(self, coalitions, epochs, early_stopping):
+        eng = self.eng
+        st = self.prepare(coalitions, epochs)
+        C = st.C
+        sizes = eng.partner_sizes
+        fed = [ci for ci in range(C) if not st.coal_is_single[ci]]
+        use_es = early_stopping and epochs > PATIENCE
+        epochs_done = np.full(C, epochs, dtype=np.int64)
+        val_hist = [[] for _ in range(C)]
+        es_best = np.full(C, np.inf)
+        es_wait = np.zeros(C, dtype=np.int64)
+        spe = {ci: -(-sizes[coalitions[ci][0]] // eng.batch_sizes[coalitions[ci][0]])
+               for ci in range(C) if st.coal_is_single[ci]}
+        per_epoch_fed = eng.minibatch_count * st.round_len
+        for s in range(st.total_steps):
+            if use_es and st.fed_steps and s % per_epoch_fed == 0 and s < st.fed_steps:
+                live = [ci for ci in fed if not st.stopped[ci]]
+                if live:  # val loss of each live global model at the start of epoch e (minibatch 0)
+                    for ci, l in zip(live, self._val_loss(st.glob, live)):
+                        val_hist[ci].append(l)
+            st.step(s)
+            if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                st.aggregate()
+                if use_es and (s + 1) % per_epoch_fed == 0:
+                    e = (s + 1) // per_epoch_fed - 1
+                    for ci in fed:
+                        if not st.stopped[ci] and e >= PATIENCE and val_hist[ci][e] > val_hist[ci][e - PATIENCE]:
+                            epochs_done[ci] = e + 1
+                            st.stop(ci)
+            if use_es and spe:
+                # singleton epoch ends: Keras EarlyStopping(monitor='val_loss', patience=10, min_delta=0)
+                ends = [ci for ci in spe if not st.stopped[ci] and (s + 1) % spe[ci] == 0
+                        and (s + 1) // spe[ci] <= epochs]
+                if ends:
+                    for ci, l in zip(ends, self._val_loss(st.params, [st.coal_first[c] for c in ends])):
+                        e = (s + 1) // spe[ci] - 1
+                        if l < es_best[ci]:
+                            es_best[ci], es_wait[ci] = l, 0
+                        else:
+                            es_wait[ci] += 1
+                            if es_wait[ci] >= PATIENCE:
+                                epochs_done[ci] = e + 1
+                                st.stop(ci)
+            if st.stopped.all():
+                break
+        glob = st.finalize()
+        correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
+        return correct / float(eng.y_test_d.numel()), epochs_done
+
+    # --------------------------------------------------------------------------------------------
+    def _evaluate(self, params, rows, x, y):
+        import torch
+        dev = self.eng.device
+        stream = _native.stream_handle(dev)
+        n = int(y.numel())
+        sel = params if rows == list(range(params.shape[0])) else params[torch.tensor(rows, device=dev)].contiguous()
+        C = sel.shape[0]
+        budget = self.eng.eval_budget_bytes
+        chunk = int(max(32, min(n, budget // max(1, C * (FEAT + HID) * 4))))
+        chunk = min(chunk, 65535)
+        pooled = torch.empty((C, chunk, FEAT), dtype=torch.float32, device=dev)
+        hidden = torch.empty((C, chunk, HID), dtype=torch.float32, device=dev)
+        correct = torch.zeros(C, dtype=torch.int32, device=dev)
+        loss = torch.zeros(C, dtype=torch.float64, device=dev)
+        _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n, chunk,
+                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(correct),
+                                                 _native.ptr(loss), stream), "mplc_cnn_evaluate")
+        return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
+
+    def _val_loss(self, params, rows):
+        _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)
+        return [float(v) for v in loss]

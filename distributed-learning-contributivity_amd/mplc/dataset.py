@@ -1,0 +1,146 @@
+"""Datasets on the coalition path (mplc/dataset.py:37-106, 397-488).
+
+Dataset keeps the reference's contract (name, input_shape, num_classes, x_/y_{train,val,test},
+train_val_split_global 90/10 with random_state 42, shorten_dataset_proportion with np.random.seed(42),
+local train/test and train/val splits for partners) so partner partitions are index-identical to the
+reference's (tests/test_scenario.py against tests/golden/splits.json).
+
+The images themselves: MNIST is loaded from a local keras-format ``mnist.npz`` (x_train, y_train,
+x_test, y_test) found via $MPLC_DATA_DIR, ./data or ~/.keras/datasets - the reference downloads it
+(mplc/dataset.py:415-440), which is impossible offline.  Without a local file, ``Mnist(synthetic=True)``
+builds tensors of MNIST's exact shapes (x ~ U[0,1) float32 [60000,28,28,1], one-hot labels) for
+throughput work; ``synthetic`` records which one was used.
+"""
+import os
+
+import numpy as np
+from sklearn.model_selection import train_test_split
+
+from . import constants
+
+
+class Dataset:
+    def __init__(self, dataset_name, input_shape, num_classes, x_train, y_train, x_test, y_test):
+        self.name = dataset_name
+        self.input_shape = input_shape
+        self.num_classes = num_classes
+        self.x_train = x_train
+        self.x_val = None
+        self.x_test = x_test
+        self.y_train = y_train
+        self.y_val = None
+        self.y_test = y_test
+        # row ids of x_train in the ORIGINAL array, kept through the global splits (engine bookkeeping)
+        self.train_rows = np.arange(len(x_train))
+        self.train_val_split_global()
+
+    def train_val_split_global(self):
+        """mplc/dataset.py:62-69: 90/10 train/val, random_state=42."""
+        if self.x_val is not None or self.y_val is not None:
+            raise Exception("x_val and y_val should be of NoneType")
+        ids = np.arange(len(self.x_train))
+        tr, va = train_test_split(ids, test_size=0.1, random_state=42)
+        self.x_train, self.x_val = self.x_train[tr], self.x_train[va]
+        self.y_train, self.y_val = self.y_train[tr], self.y_train[va]
+
+    @staticmethod
+    def train_test_split_local(x, y):
+        return x, np.array([]), y, np.array([])
+
+    @staticmethod
+    def train_val_split_local(x, y):
+        return x, np.array([]), y, np.array([])
+
+    def generate_new_model(self):
+        raise NotImplementedError("models are built by the engine's batched kernels (mplc.engine)")
+
+    def shorten_dataset_proportion(self, dataset_proportion):
+        """mplc/dataset.py:83-106."""
+        if dataset_proportion == 1:
+            return
+        if dataset_proportion < 0:
+            raise ValueError("The dataset proportion should be strictly between 0 and 1")
+        skip_train_idx = int(round(len(self.x_train) * dataset_proportion))
+        train_idx = np.arange(len(self.x_train))
+        skip_val_idx = int(round(len(self.x_val) * dataset_proportion))
+        val_idx = np.arange(len(self.x_val))
+        np.random.seed(42)
+        np.random.shuffle(train_idx)
+        np.random.shuffle(val_idx)
+        self.x_train = self.x_train[train_idx[0:skip_train_idx]]
+        self.y_train = self.y_train[train_idx[0:skip_train_idx]]
+        self.x_val = self.x_val[val_idx[0:skip_val_idx]]
+        self.y_val = self.y_val[val_idx[0:skip_val_idx]]
+
+
+def _local_mnist():
+    dirs = [os.environ.get("MPLC_DATA_DIR", ""), os.path.join(os.getcwd(), "data"),
+            os.path.expanduser("~/.keras/datasets")]
+    for d in dirs:
+        p = os.path.join(d, "mnist.npz") if d else ""
+        if p and os.path.exists(p):
+            with np.load(p, allow_pickle=False) as f:
+                return (f["x_train"], f["y_train"]), (f["x_test"], f["y_test"])
+    return None
+
+
+def _one_hot(y, k):
+    return np.eye(k, dtype="float32")[np.asarray(y, dtype=np.int64).ravel()]
+
+
+class Mnist(Dataset):
+    """mplc/dataset.py:397-488 (model: the engine's batched CNN of the same architecture)."""
+
+    def __init__(self, synthetic=None, seed=0, n_train=60000, n_test=10000):
+        self.img_rows = self.img_cols = 28
+        loaded = None if synthetic else _local_mnist()
+        if loaded is None:
+            if synthetic is False:
+                raise FileNotFoundError("mnist.npz not found (set MPLC_DATA_DIR); no network to download it")
+            rng = np.random.default_rng(seed)
+            x_train = rng.random((n_train, 28, 28, 1), dtype=np.float32)
+            x_test = rng.random((n_test, 28, 28, 1), dtype=np.float32)
+            y_train = _one_hot(rng.integers(0, 10, n_train), 10)
+            y_test = _one_hot(rng.integers(0, 10, n_test), 10)
+            self.synthetic = True
+        else:
+            (xt, yt), (xs, ys) = loaded
+            x_train = (xt.reshape(xt.shape[0], 28, 28, 1).astype("float32") / 255)
+            x_test = (xs.reshape(xs.shape[0], 28, 28, 1).astype("float32") / 255)
+            y_train, y_test = _one_hot(yt, 10), _one_hot(ys, 10)
+            self.synthetic = False
+        super().__init__("mnist", (28, 28, 1), 10, x_train, y_train, x_test, y_test)
+
+    @staticmethod
+    def train_test_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+    @staticmethod
+    def train_val_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+
+class ArrayDataset(Dataset):
+    """An MNIST-shaped dataset from caller arrays (tests, sklearn digits upsampled, private data).
+    Uses the MNIST local splits (train_test_split 0.1, random_state 42, twice)."""
+
+    def __init__(self, x_train, y_train, x_test, y_test, name="mnist", num_classes=10):
+        super().__init__(name, (28, 28, 1), num_classes, x_train, y_train, x_test, y_test)
+
+    train_test_split_local = staticmethod(Mnist.train_test_split_local)
+    train_val_split_local = staticmethod(Mnist.train_val_split_local)
+
+
+def digits_as_mnist(seed=0):
+    """sklearn's bundled 8x8 digits (no network) upsampled x3 and padded to 28x28, values / 16:
+    a small real, learnable MNIST-shaped dataset for accuracy tests.  Returns (x, y_onehot)."""
+    from sklearn.datasets import load_digits
+    d = load_digits()
+    x = d.images.astype(np.float32) / 16.0
+    x = np.kron(x, np.ones((3, 3), dtype=np.float32))
+    x = np.pad(x, ((0, 0), (2, 2), (2, 2)))[..., None]
+    y = _one_hot(d.target, 10)
+    return x, y
+
+
+__all__ = ["Dataset", "Mnist", "ArrayDataset", "digits_as_mnist", "constants"]

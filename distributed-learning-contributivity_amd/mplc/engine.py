@@ -1,0 +1,148 @@
+"""Coalition-evaluation engine: v(S) for many coalitions at once on the MI355X.
+
+Replaces the reference's one-coalition-at-a-time loop (Contributivity.not_twice_characteristic ->
+FederatedAverageLearning/SinglePartnerLearning(...).fit() -> history.score,
+mplc/contributivity.py:92-136, mplc/multi_partner_learning.py:195-334) with batched training of every
+requested coalition in lockstep (mplc/cnn.py, csrc/mnist_cnn.hip).
+
+Data live in HBM for the engine's lifetime: the dataset's train/val/test arrays (fp32 images, int32
+labels), and each partner's row indices into the train array (the reference's partner.x_train copies,
+mplc/scenario.py:571-681).
+
+Determinism: v(S) depends only on (S, seed) - initial weights are keyed by (seed, S) and each
+replica's sample order by (seed, S, partner, epoch, round) - so a coalition evaluated alone or inside
+any batch, on any GPU, gets the same value.  (The reference's values are not reproducible at all:
+TF is never seeded, mplc/scenario.py:614 only seeds numpy for the split.)
+"""
+import os
+
+import numpy as np
+
+from . import constants
+from .cnn import CnnBatchTrainer, minibatch_bounds, STRIDE, FEAT, HID, W1P, W2P
+
+
+class CoalitionEngine:
+    """Batched v(S) evaluator bound to one scenario's partners, data and training hyper-parameters."""
+
+    def __init__(self, *, x_train, y_train, x_val, y_val, x_test, y_test, partner_rows, batch_sizes,
+                 epoch_count, minibatch_count, aggregation="data-volume", is_early_stopping=True, seed=0,
+                 model="mnist_cnn", device=None, memory_budget_bytes=None, eval_budget_bytes=8 << 30):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("MI355X (HIP) device required: the MPLC engine has no CPU fallback")
+        if model != "mnist_cnn":
+            raise NotImplementedError(f"model '{model}' has no batched MI355X kernels yet (see DESIGN.md)")
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.model = model
+        self.seed = int(seed)
+        self.epoch_count = int(epoch_count)
+        self.minibatch_count = int(minibatch_count)
+        self.aggregation = aggregation
+        self.is_early_stopping = bool(is_early_stopping)
+        self.eval_budget_bytes = int(eval_budget_bytes)
+
+        def images(x):
+            x = np.asarray(x, dtype=np.float32)
+            return torch.from_numpy(np.ascontiguousarray(x.reshape(x.shape[0], 28, 28))).to(self.device)
+
+        def labels(y):
+            y = np.asarray(y)
+            if y.ndim == 2:
+                y = np.argmax(y, axis=1)  # one-hot (keras.utils.to_categorical) -> class id
+            return torch.from_numpy(np.ascontiguousarray(y.astype(np.int32))).to(self.device)
+
+        self.x_train_d, self.y_train_d = images(x_train), labels(y_train)
+        self.x_val_d, self.y_val_d = images(x_val), labels(y_val)
+        self.x_test_d, self.y_test_d = images(x_test), labels(y_test)
+        self.partner_sizes = [int(len(r)) for r in partner_rows]
+        self.batch_sizes = [int(b) for b in batch_sizes]
+        rows, splits, self.rows_off, self.split_off, self.bounds = [], [], [], [], []
+        for r in partner_rows:
+            self.rows_off.append(len(rows))
+            rows.extend(int(i) for i in r)
+            b = minibatch_bounds(len(r), self.minibatch_count)
+            self.bounds.append(b)
+            self.split_off.append(len(splits))
+            splits.extend(b)
+        self.rows_d = torch.tensor(rows, dtype=torch.int32, device=self.device)
+        self.splits_d = torch.tensor(splits, dtype=torch.int32, device=self.device)
+        if memory_budget_bytes is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            memory_budget_bytes = int(free * 0.8) - self.eval_budget_bytes
+        self.memory_budget_bytes = int(memory_budget_bytes)
+        self.trainer = CnnBatchTrainer(self)
+        self.stats = {"coalitions": 0, "batches": 0, "replicas": 0}
+
+    # --------------------------------------------------------------------------------------------
+    @classmethod
+    def for_scenario(cls, scenario, **overrides):
+        ds = scenario.dataset
+        name = getattr(ds, "name", "mnist")
+        model = {"mnist": "mnist_cnn"}.get(name, name)
+        parts = scenario.partners_list
+        rows = []
+        for p in parts:
+            if getattr(p, "train_idx", None) is None:
+                raise ValueError("partners need train_idx (row indices into dataset.x_train); use mplc.scenario")
+            rows.append(np.asarray(p.train_idx))
+        kw = dict(x_train=ds.x_train, y_train=ds.y_train, x_val=ds.x_val, y_val=ds.y_val, x_test=ds.x_test,
+                  y_test=ds.y_test, partner_rows=rows, batch_sizes=[int(p.batch_size) for p in parts],
+                  epoch_count=scenario.epoch_count, minibatch_count=scenario.minibatch_count,
+                  aggregation=getattr(scenario, "aggregation_weighting", "data-volume"),
+                  is_early_stopping=getattr(scenario, "is_early_stopping", True),
+                  seed=getattr(scenario, "engine_seed", int(os.environ.get("MPLC_ENGINE_SEED", "0"))), model=model)
+        kw.update(overrides)
+        return cls(**kw)
+
+    # --------------------------------------------------------------------------------------------
+    def replica_bytes(self, bmax):
+        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + bmax * W1P * 4 + 4 * W2P * 4
+                + 9 * 64 * 32 * 4 + bmax * 12)
+
+    def plan_batches(self, coalitions):
+        """Split coalitions into lockstep batches that fit the HBM budget (cost-sorted so that a batch holds
+        coalitions of similar size; every coalition's replicas stay together)."""
+        order = sorted(range(len(coalitions)), key=lambda i: (len(coalitions[i]) == 1, -len(coalitions[i])))
+        batches, cur, cur_bytes = [], [], 0
+        for i in order:
+            c = coalitions[i]
+            bmax = max(self.batch_sizes[p] for p in c)
+            need = len(c) * self.replica_bytes(bmax) + STRIDE * 4
+            if cur and (cur_bytes + need > self.memory_budget_bytes or len(cur) >= 65535):
+                batches.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(i)
+            cur_bytes += need
+        if cur:
+            batches.append(cur)
+        return batches
+
+    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):
+        """v(S) (test accuracy, float64) for each coalition (sorted tuple of partner indices)."""
+        coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
+        for c in coalitions:
+            if len(c) == 0 or c[0] < 0 or c[-1] >= len(self.partner_sizes) or len(set(c)) != len(c):
+                raise ValueError(f"invalid coalition {c}")
+        E = self.epoch_count if epoch_count is None else int(epoch_count)
+        es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
+        scores = np.zeros(len(coalitions))
+        epochs_done = np.zeros(len(coalitions), dtype=np.int64)
+        for batch in self.plan_batches(coalitions):
+            coal = [coalitions[i] for i in batch]
+            s, e = self.trainer.run(coal, E, es)
+            scores[batch] = s
+            epochs_done[batch] = e
+            self.stats["batches"] += 1
+            self.stats["replicas"] += sum(len(c) for c in coal)
+        self.stats["coalitions"] += len(coalitions)
+        if return_details:
+            return {"scores": scores, "epochs_done": epochs_done}
+        return scores
+
+
+def default_seed():
+    return int(os.environ.get("MPLC_ENGINE_SEED", "0"))
+
+
+__all__ = ["CoalitionEngine", "constants"]

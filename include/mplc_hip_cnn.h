@@ -1,6 +1,26 @@
 /*
- * mplc_hip_cnn.h - batched multi-model CNN trainer entry points (part of the mplc_hip.h C ABI).
- * Populated as the trainer kernels land; see mplc_hip.h for conventions.
+ * mplc_hip_cnn.h - batched multi-model MNIST CNN trainer (part of the mplc_hip.h C ABI).
+ *
+ * Model (mplc/dataset.py:457-479): Conv2D(32,3x3,relu) -> Conv2D(64,3x3,relu) -> MaxPool(2) -> Flatten
+ * -> Dense(128,relu) -> Dense(10,softmax); categorical cross-entropy; Keras 2.3.1 Adam (lr 1e-3,
+ * beta 0.9/0.999, eps 1e-7); glorot_uniform kernels, zero biases.
+ *
+ * A MODEL is one flat fp32 parameter row of MPLC_CNN_STRIDE floats (Keras weight order per layer:
+ * conv kernels [kh][kw][cin][cout], dense [in][out]; offsets below).  A REPLICA is one model being
+ * trained on one partner's data: a (coalition, partner) pair of a FedAvg coalition or the single model
+ * of a singleton coalition.  B replicas step in lockstep; each has its own batch size, sample schedule
+ * and Adam step count (ragged batches are masked per replica).
+ *
+ * Replaces, for all replicas at once:
+ *   - Keras `model.fit(x_mb, y_mb, batch_size=bs_p, epochs=1)` per partner per FedAvg round with a fresh
+ *     optimizer (mplc/multi_partner_learning.py:301-332, partner.build_model mplc/partner.py:169-170),
+ *   - the singleton `model.fit(x, y, batch_size=bs_p, epochs=E)` with persistent Adam
+ *     (mplc/multi_partner_learning.py:253-260),
+ *   - `model.evaluate(x, y, batch_size=256)` -> [loss, accuracy] (mplc/multi_partner_learning.py:142-169).
+ * Sample order: epoch permutation of the partner's rows (PartnerMpl.split_minibatches,
+ * mplc/partner.py:155-167), split at floor(k/M * n_p), then Keras' per-fit shuffle inside the minibatch;
+ * both permutations are keyed bijections so v(S) is a deterministic function of
+ * (S, seed) whatever the batch composition.
  */
 #ifndef MPLC_HIP_CNN_H
 #define MPLC_HIP_CNN_H
@@ -11,6 +31,95 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* parameter row layout (floats) */
+#define MPLC_CNN_OFF_W1 0          /* 3*3*1*32   */
+#define MPLC_CNN_OFF_B1 288        /* 32         */
+#define MPLC_CNN_OFF_W2 320        /* 3*3*32*64  */
+#define MPLC_CNN_OFF_B2 18752      /* 64         */
+#define MPLC_CNN_OFF_W3 18816      /* 9216*128   */
+#define MPLC_CNN_OFF_B3 1198464    /* 128        */
+#define MPLC_CNN_OFF_W4 1198592    /* 128*10     */
+#define MPLC_CNN_OFF_B4 1199872    /* 10         */
+#define MPLC_CNN_NPARAM 1199882
+#define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
+#define MPLC_CNN_FEAT 9216         /* flattened pooled features */
+#define MPLC_CNN_HID 128
+#define MPLC_CNN_NCLS 10
+#define MPLC_CNN_W1P 320           /* per-sample partial gradient of W1+b1 */
+#define MPLC_CNN_W2P 18496         /* partial gradient row of W2+b2 */
+
+/* replica kinds */
+#define MPLC_REP_IDLE (-1)
+#define MPLC_REP_FEDAVG 0     /* member of a FedAvg coalition: M rounds per epoch, fresh Adam per round */
+#define MPLC_REP_SINGLE 1     /* singleton coalition: Keras fit over all rows, E epochs, persistent Adam  */
+
+typedef struct {
+  int32_t kind;       /* MPLC_REP_*                                                      */
+  int32_t n_rows;     /* partner train size n_p                                          */
+  int32_t batch;      /* partner batch size bs_p (mplc/scenario.py:705-724)              */
+  int32_t rows_off;   /* offset of the partner's dataset row indices in `rows`           */
+  int32_t split_off;  /* offset of the partner's M+1 minibatch boundaries in `splits`    */
+  int32_t model;      /* index of the replica's parameter row                            */
+  uint64_t key;       /* shuffle key (seed, coalition, partner)                          */
+} mplc_replica_t;     /* 32 bytes */
+
+typedef struct {
+  /* geometry */
+  int32_t n_rep;          /* replicas                                                     */
+  int32_t bmax;           /* max batch size over replicas (slot stride)                   */
+  int32_t w2_splits;      /* = ceil(bmax / 8): wgrad splits of 8 samples per replica      */
+  int32_t pad0;
+  /* schedule (global step -> per-replica samples) */
+  int32_t step;           /* global step index                                            */
+  int32_t minibatch_count;/* M                                                            */
+  int32_t round_len;      /* steps per FedAvg round (max over replicas)                   */
+  int32_t epochs;         /* E                                                            */
+  const mplc_replica_t* reps;
+  const int32_t* rows;    /* concatenated partner row indices into x/labels               */
+  const int32_t* splits;  /* concatenated minibatch boundaries, M+1 per partner           */
+  /* data */
+  const float* x;         /* [N][28][28] fp32 in [0,1]                                    */
+  const int32_t* labels;  /* [N] class ids                                                */
+  /* model state */
+  float* params;          /* [n_rep][MPLC_CNN_STRIDE]                                     */
+  float* adam_m;
+  float* adam_v;
+  /* workspaces (device) */
+  int32_t* idx;           /* [n_rep][bmax]                                                */
+  int32_t* cnt;           /* [n_rep]                                                      */
+  int32_t* adam_t;        /* [n_rep]  (0 = idle this step)                                */
+  float* pooled;          /* [n_rep][bmax][9216]                                          */
+  uint8_t* code;          /* [n_rep][bmax][9216] argmax-in-window | 0x80 if positive      */
+  float* hidden;          /* [n_rep][bmax][128]                                           */
+  float* dhidden;         /* [n_rep][bmax][128]                                           */
+  float* dpooled;         /* [n_rep][bmax][9216]                                          */
+  float* w1_part;         /* [n_rep][bmax][MPLC_CNN_W1P]                                  */
+  float* w2_part;         /* [n_rep][w2_splits][MPLC_CNN_W2P]                             */
+  float* w2t;             /* [n_rep][9*64*32] W2 transposed for the data-gradient MFMA    */
+  /* optimizer (Keras 2.3.1 Adam) */
+  float lr, beta1, beta2, eps;
+} mplc_cnn_train_t;
+
+/* Parameter row stride in floats (== MPLC_CNN_STRIDE). */
+int mplc_cnn_stride(void);
+
+/* glorot_uniform kernels / zero biases for n_models rows, keyed per model (deterministic counter RNG). */
+int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream);
+
+/* dst[i] = src[map[i]] row copies (start of training: replica rows <- coalition global rows). */
+int mplc_cnn_copy_rows(float* dst, const float* src, int64_t stride, const int32_t* map, int n_rows,
+                       void* stream);
+
+/* Enqueue one lockstep training step of all replicas (schedule, forward, backward, Adam). */
+int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream);
+
+/* Forward-only evaluation of n_models models on samples [0, n_samples) of x/labels:
+ * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  pooled/hidden are
+ * workspaces of n_models * chunk * 9216 and n_models * chunk * 128 floats. */
+int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
+                      int n_samples, int chunk, float* pooled, float* hidden, int32_t* correct, double* loss_sum,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,11 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_shapley.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_shapley -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_shapley.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc $rc" >> gpurun_out/pytest_gpu.log
+if [ $rc -gt 1 ]; then echo "stop after pytest rc $rc"; exit $rc; fi
+timeout -k 10 300 python scripts/probe_train.py 64 1 5 > gpurun_out/probe.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python scripts/probe_train.py 64 1 5 > gpurun_out/prof_train.log 2>&1
 echo EXIT $?

@@ -1,0 +1,212 @@
+"""GPU parity of the batched MNIST-CNN trainer against the torch-CPU oracle (oracle/cnn.py).
+
+Integer/index work (initial weights from the keyed counter, the sample schedule) must be bit-exact.
+Floating point: gradients of one step within 2e-4 relative (fp32, different summation order), forward
+activations within 1e-4; trained coalition accuracies within +-1 point on average (the reference's own
+tolerance for "accuracies within 1 pt"), each within 3 points (small test set: 1 sample = 0.34 pt).
+Data: sklearn's bundled digits upsampled to 28x28 (mplc.dataset.digits_as_mnist) - real, learnable,
+MNIST-shaped, no network."""
+import numpy as np
+import pytest
+
+from oracle import cnn as ocnn
+
+pytestmark = pytest.mark.gpu
+
+
+def make_scenario(partners=3, amounts=(0.2, 0.5, 0.3), M=2, G=4, E=2, es=False):
+    from mplc.dataset import ArrayDataset, digits_as_mnist
+    from mplc.scenario import Scenario
+    x, y = digits_as_mnist()
+    ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:])
+    sc = Scenario(partners, list(amounts), dataset=ds, minibatch_count=M, gradient_updates_per_pass_count=G,
+                  epoch_count=E, is_early_stopping=es)
+    return sc.provision()
+
+
+@pytest.fixture(scope="module")
+def scenario():
+    return make_scenario()
+
+
+@pytest.fixture(scope="module")
+def engine(scenario):
+    from mplc.engine import CoalitionEngine
+    return CoalitionEngine.for_scenario(scenario, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
+
+
+@pytest.fixture(scope="module")
+def odata(scenario):
+    ds = scenario.dataset
+    return ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+
+
+def rows(scenario):
+    return [p.train_idx for p in scenario.partners_list], [p.batch_size for p in scenario.partners_list]
+
+
+def test_init_params_bit_exact(engine):
+    st = engine.trainer.prepare([(0, 2), (1,)], 1)
+    g = st.glob.cpu().numpy()
+    for ci, c in enumerate([(0, 2), (1,)]):
+        ref = ocnn.init_params(ocnn.init_key(engine.seed, sum(1 << p for p in c)))
+        assert np.array_equal(g[ci], ref)
+    # replica rows start from their coalition's row
+    p = st.params.cpu().numpy()
+    assert np.array_equal(p[0], g[0]) and np.array_equal(p[1], g[0]) and np.array_equal(p[2], g[1])
+
+
+def test_schedule_bit_exact(scenario, engine):
+    import torch
+    prow, bs = rows(scenario)
+    coal = [(0, 1, 2), (2,)]
+    st = engine.trainer.prepare(coal, 2)
+    M = engine.minibatch_count
+    for s in (0, 1, st.round_len, st.round_len * M + 3):
+        st.step(s)
+        torch.cuda.synchronize()
+        idx = st.ws["idx"].cpu().numpy()
+        cnt = st.ws["cnt"].cpu().numpy()
+        e, rem = divmod(s, M * st.round_len)
+        m, t = divmod(rem, st.round_len)
+        for r, p in enumerate((0, 1, 2)):
+            steps = ocnn.fedavg_round_rows(ocnn.shuffle_key(engine.seed, 0b111, p), prow[p], bs[p], M, e, m)
+            expect = steps[t] if t < len(steps) else np.array([], dtype=np.int64)
+            assert cnt[r] == len(expect)
+            assert idx[r, :cnt[r]].tolist() == [int(v) for v in expect]
+        spe = -(-len(prow[2]) // bs[2])
+        es_, ts = divmod(s, spe)
+        srows = ocnn.single_epoch_rows(ocnn.shuffle_key(engine.seed, 0b100, 2), prow[2], bs[2], es_)[ts]
+        assert idx[3, :cnt[3]].tolist() == [int(v) for v in srows]
+
+
+def test_one_step_gradients_and_activations(scenario, engine, odata):
+    """lr = 0: Adam's first moment after step 1 is (1 - beta1) * g, which exposes the device gradient."""
+    import torch
+    coal = [(0, 1), (1, 2)]
+    st = engine.trainer.prepare(coal, 1)
+    st.t.lr = 0.0
+    p0 = st.params.cpu().numpy().copy()
+    st.step(0)
+    torch.cuda.synchronize()
+    idx = st.ws["idx"].cpu().numpy()
+    cnt = st.ws["cnt"].cpu().numpy()
+    m = st.adam_m.cpu().numpy()
+    pooled = st.ws["pooled"].cpu().numpy()
+    hidden = st.ws["hidden"].cpu().numpy()
+    assert np.array_equal(st.params.cpu().numpy(), p0)  # lr = 0: no update
+    for r in range(st.R):
+        rws = idx[r, :cnt[r]]
+        P = ocnn.unpack(p0[r])
+        x = odata.x_train[rws]
+        y = odata.y_train[rws]
+        grads, _ = ocnn.gradients(P, x, y)
+        g_dev = m[r] / np.float32(0.1)
+        for name, (off, shape) in ocnn.OFF.items():
+            n = int(np.prod(shape))
+            gd = g_dev[off:off + n]
+            gr = grads[name].numpy().reshape(-1)
+            err = np.linalg.norm(gd - gr) / max(np.linalg.norm(gr), 1e-12)
+            assert err < 2e-4, (r, name, err)
+        # activations
+        F = torch.nn.functional
+        with torch.no_grad():
+            h = F.relu(F.conv2d(x.unsqueeze(1), P["W1"].permute(3, 2, 0, 1), P["b1"]))
+            h = F.max_pool2d(F.relu(F.conv2d(h, P["W2"].permute(3, 2, 0, 1), P["b2"])), 2)
+            flat = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1).numpy()
+            hid = np.maximum(flat @ P["W3"].numpy() + P["b3"].numpy(), 0)
+        assert np.max(np.abs(pooled[r, :cnt[r]] - flat)) <= 1e-4 * max(1.0, np.max(np.abs(flat)))
+        assert np.max(np.abs(hidden[r, :cnt[r]] - hid)) <= 1e-4 * max(1.0, np.max(np.abs(hid)))
+
+
+def test_one_adam_step_matches_keras_adam(scenario, engine, odata):
+    import torch
+    coal = [(0, 2)]
+    st = engine.trainer.prepare(coal, 1)
+    p0 = st.params.cpu().numpy().copy()
+    st.step(0)
+    torch.cuda.synchronize()
+    idx, cnt = st.ws["idx"].cpu().numpy(), st.ws["cnt"].cpu().numpy()
+    p1 = st.params.cpu().numpy()
+    for r in range(st.R):
+        P = ocnn.unpack(p0[r])
+        rws = idx[r, :cnt[r]]
+        g, _ = ocnn.gradients(P, odata.x_train[rws], odata.y_train[rws])
+        opt = ocnn.KerasAdam(P)
+        opt.step(P, g)
+        ref = ocnn.pack(P)
+        d_dev = p1[r, :ocnn.STRIDE] - p0[r]
+        d_ref = ref - p0[r]
+        # first Adam step moves every weight by ~lr * sign(g); allow sign flips only where |g| ~ noise
+        diff = np.abs(d_dev - d_ref)
+        assert np.mean(diff) < 2e-6
+        assert np.mean(diff > 1e-5) < 2e-3
+
+
+def test_fedavg_aggregation_inside_training_is_np_average(scenario, engine):
+    import torch
+    st = engine.trainer.prepare([(0, 1, 2)], 1)
+    for s in range(st.round_len):
+        st.step(s)
+    before = st.params.cpu().numpy().copy()
+    st.aggregate()
+    torch.cuda.synchronize()
+    sizes = [engine.partner_sizes[p] for p in (0, 1, 2)]
+    w = np.asarray(sizes) / np.sum(sizes)
+    ref = np.average(before[:, :ocnn.STRIDE], axis=0, weights=w).astype(np.float32)
+    assert np.array_equal(st.glob.cpu().numpy()[0], ref)
+    after = st.params.cpu().numpy()
+    for r in range(3):
+        assert np.array_equal(after[r], ref)  # broadcast: every partner starts the next round from it
+
+
+def test_values_independent_of_batch_composition(engine):
+    all7 = [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
+    together = engine.evaluate(all7)
+    alone = [engine.evaluate([c])[0] for c in ((1, 2), (2,))]
+    assert together[5] == alone[0] and together[2] == alone[1]
+
+
+def test_coalition_accuracies_vs_oracle(scenario, engine, odata):
+    prow, bs = rows(scenario)
+    all7 = [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
+    dev = engine.evaluate(all7)
+    ref = np.array([ocnn.coalition_value(odata, prow, bs, c, seed=engine.seed, epochs=engine.epoch_count,
+                                         M=engine.minibatch_count)[0] for c in all7])
+    diff = np.abs(dev - ref)
+    assert np.mean(diff) <= 0.01, (dev, ref)
+    assert np.max(diff) <= 0.03, (dev, ref)
+    assert np.all(dev > 0.5)  # models learn (10 classes: chance = 0.1)
+
+
+def test_partner_ranking_reference_contrib_test():
+    """Port of tests/end_to_end_tests.py:54-73: partner with 10% of the data scores below the 90% partner for
+    both "Shapley values" and "Independent scores" (MNIST-shaped data, E=1, M=10, G=8 as the contrib yml)."""
+    from mplc.contributivity import Contributivity
+    sc = make_scenario(partners=2, amounts=(0.1, 0.9), M=10, G=8, E=1)
+    for method in ("Shapley values", "Independent scores"):
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity(method)
+        assert c.contributivity_scores[0] < c.contributivity_scores[1], (method, c.contributivity_scores)
+        assert c.first_charac_fct_calls_count == (3 if method == "Shapley values" else 2)
+
+
+def test_scenario_run_end_to_end():
+    sc = make_scenario(partners=3, amounts=(0.2, 0.5, 0.3), M=2, G=4, E=2)
+    sc.methods = ["Shapley values", "Independent scores", "TMCS"]
+    sc.run()
+    df = sc.to_dataframe()
+    assert len(df) == 9
+    assert sc.mpl.history.score > 0.5
+    sv = sc.contributivity_list[0]
+    assert abs(np.sum(sv.contributivity_scores) - sc.mpl.history.score) < 1e-9  # efficiency: sum SV = v(N)
+
+
+def test_early_stopping_path_runs():
+    """E > PATIENCE with early stopping: val evals per epoch, coalitions may stop; epochs_done recorded."""
+    from mplc.engine import CoalitionEngine
+    sc = make_scenario(partners=2, amounts=(0.5, 0.5), M=1, G=2, E=12, es=True)
+    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    res = eng.evaluate([(0,), (0, 1)], return_details=True)
+    assert np.all(res["epochs_done"] >= 1) and np.all(res["epochs_done"] <= 12)
+    assert np.all(res["scores"] > 0.5)
