@@ -1,10 +1,18 @@
 """Benchmark driver (contract: one JSON line on rank 0).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--leg shapley|train]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--leg train|shapley]
 
-leg "shapley": exact-Shapley aggregation of a synthetic N=28 v(S) table (2^28 fp64 = 2 GiB, resident
-in HBM before timing), range-sharded across ranks, partial sums all-reduced over RCCL.  One step = one
-full aggregation.  metric = algorithmic GB/s (8 bytes per mask read once).
+leg "train" (default; BASELINE.json metric "coalition v(S) evals/sec (MNIST FedAvg)"): BASELINE config #3
+  - MNIST CNN, 10 partners, random split ([0.1]*10), FedAvg, exact "Shapley values" over all 1023
+  coalitions, M=20 minibatches, G=8 gradient updates per pass, fixed E=2 epochs (no early stopping, so
+  the work is deterministic).  MNIST-shaped synthetic data (x ~ U[0,1) fp32
+  [60000,28,28,1], random one-hot labels; no network for the dataset), resident in HBM before timing.
+  One step = one full Contributivity.compute_contributivity("Shapley values"): train + test-evaluate all
+  1023 coalitions (batched, lockstep), then the exact-Shapley aggregation.  value = coalitions / second.
+  Multi-GPU: coalitions LPT-sharded over ranks, v(S) assembled by one RCCL all_reduce (strong scaling:
+  the job is fixed).
+  Also reported: "shapley_agg" - the exact-Shapley aggregation kernel on a 2^28 fp64 table (config #5).
+leg "shapley": only the N=28 aggregation (GB/s).
 """
 import argparse
 import json
@@ -18,7 +26,9 @@ for _p in (REPO, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (v_mfma_f32_32x32x2_f32), spec
+CONV_BWD_DATA_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2  # dA1 = dZ2 (*) W2 over all conv1 positions
 
 
 def dist_init():
@@ -51,6 +61,19 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def sum_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# --------------------------------------------------------------------------------------------------
+# exact-Shapley aggregation (config #5)
+# --------------------------------------------------------------------------------------------------
 def make_synthetic_table_device(n, begin, end, device):
     """Section 8(d) synthetic table restricted to masks [begin, end), generated on device (not timed)."""
     import numpy as np
@@ -69,12 +92,51 @@ def make_synthetic_table_device(n, begin, end, device):
     return V.contiguous()
 
 
+def bench_shapley(n, steps, warmup, rank, world):
+    import torch
+    import torch.distributed as dist
+    from mplc.shapley import ShapleyAggregator, shard_range
+    begin, end = shard_range(n, rank, world)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    V = make_synthetic_table_device(n, begin, end, dev)
+    agg = ShapleyAggregator(n, device=dev, count=end - begin)
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        p = agg.partial(V, begin)
+        if world > 1:
+            dist.all_reduce(p)
+        agg.finalize(p)
+    barrier(world)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        agg.partial(V, begin)
+        ev[i][1].record(stream)
+        if world > 1:
+            dist.all_reduce(agg.partial_buf)
+        agg.finalize(agg.partial_buf)
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    kern_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b in ev) / steps, world)
+    ms_per_step = wall * 1000 / steps
+    shard_bytes = (end - begin) * 8
+    achieved = shard_bytes / (kern_ms / 1000) / 1e9
+    return {
+        "metric": "exact-Shapley aggregation GB/s at N=%d" % n, "value": round((1 << n) * 8 / (ms_per_step / 1000) / 1e9, 2),
+        "unit": "GB/s", "ms_per_step": round(ms_per_step, 4), "n": n, "table_bytes": (1 << n) * 8,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "shapley_block_kernel+shapley_reduce_blocks_kernel", "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": shard_bytes},
+    }
+
+
 def cpu_baseline_shapley(n_sample=24):
-    """Oracle fp64 OpenMP single pass over a 2^24 table (bounded sample, ~128 MiB), GB/s."""
     from oracle import shapley as osh
     threads = min(16, os.cpu_count() or 1)
     V = osh.synthetic_table(n_sample)
-    osh.shapley_bitmask_f64_omp(n_sample, V, threads)  # warm
+    osh.shapley_bitmask_f64_omp(n_sample, V, threads)
     reps, t0 = 0, time.perf_counter()
     while True:
         osh.shapley_bitmask_f64_omp(n_sample, V, threads)
@@ -83,81 +145,165 @@ def cpu_baseline_shapley(n_sample=24):
             break
     dt = (time.perf_counter() - t0) / reps
     return {"value": round(V.nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp64 OpenMP single pass over a 2^{n_sample} fp64 table ({V.nbytes >> 20} MiB), "
-                      f"{reps} reps"}
+            "sample": f"oracle fp64 OpenMP single pass over a 2^{n_sample} fp64 table ({V.nbytes >> 20} MiB), {reps} reps"}
 
 
-def bench_shapley(args, rank, world):
+# --------------------------------------------------------------------------------------------------
+# training leg (config #3)
+# --------------------------------------------------------------------------------------------------
+def build_scenario(partners, epochs, M, G):
+    from mplc.dataset import Mnist
+    from mplc.scenario import Scenario
+    amounts = [1.0 / partners] * partners
+    if partners == 10:
+        amounts = [0.1] * 10
+    sc = Scenario(partners, amounts, dataset=Mnist(synthetic=True), minibatch_count=M,
+                  gradient_updates_per_pass_count=G, epoch_count=epochs, is_early_stopping=False)
+    return sc.provision()
+
+
+def cpu_baseline_train(sc, epochs, M, budget_s=25.0):
+    """Oracle (torch-CPU fp32, sequential one coalition at a time like the reference) on a bounded stratified
+    sample: one coalition of each size 1, 2, 3 (size 1 = singleton fit); per-partner cost is linear in |S|
+    for FedAvg, so the full 2^n - 1 sweep is extrapolated as sum_k C(n,k) t(k) with t(k) from a line
+    through the measured FedAvg sizes (t(1) measured directly)."""
+    import numpy as np
     import torch
-    import torch.distributed as dist
-    from mplc.shapley import ShapleyAggregator, shard_range
-    n = args.n
-    begin, end = shard_range(n, rank, world)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    V = make_synthetic_table_device(n, begin, end, dev)
-    agg = ShapleyAggregator(n, device=dev, count=end - begin)
-    stream = torch.cuda.current_stream()
+    from math import comb
+    from oracle import cnn as ocnn
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ds = sc.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    n = len(prow)
+    times = {}
+    t_all = time.perf_counter()
+    for k in (1, 2, 3):
+        t0 = time.perf_counter()
+        ocnn.coalition_value(data, prow, bs, tuple(range(k)), epochs=epochs, M=M)
+        times[k] = time.perf_counter() - t0
+        if time.perf_counter() - t_all > budget_s and k >= 2:
+            break
+    ks = sorted(k for k in times if k >= 2)
+    if len(ks) >= 2:
+        slope = (times[ks[-1]] - times[ks[0]]) / (ks[-1] - ks[0])
+        icpt = times[ks[0]] - slope * ks[0]
+    else:
+        slope, icpt = times[2] / 2.0, 0.0
+    total = sum(comb(n, k) * (times[1] if k == 1 else icpt + slope * k) for k in range(1, n + 1))
+    return {"value": round((2 ** n - 1) / total, 5), "unit": "coalition evals/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle torch-CPU fp32 sequential FedAvg/singleton fits of coalitions of size 1,2,3 "
+                       f"(E={epochs}, M={M}): {', '.join(f'|S|={k}: {v:.1f}s' for k, v in sorted(times.items()))}; "
+                       f"full {2 ** n - 1}-coalition sweep extrapolated linearly in |S|: {total:.0f}s")}
 
-    def step():
-        p = agg.partial(V, begin)
-        if world > 1:
-            dist.all_reduce(p)
-        return agg.finalize(p)
+
+def bench_train(args, rank, world):
+    import numpy as np
+    import torch
+    from mplc.contributivity import Contributivity
+    from mplc.profiling import KernelTimer
+    sc = build_scenario(args.partners, args.epochs, args.minibatches, args.gupp)
+    from mplc.engine import CoalitionEngine
+    sc.engine = CoalitionEngine.for_scenario(sc)
+    eng = sc.engine
+    eng.evaluate([(0, 1)], epoch_count=1)  # untimed: module load, allocator warm-up
+    n = args.partners
+    n_coal = 2 ** n - 1
+
+    def one_step():
+        sc.coalition_values = {}  # retrain every coalition each step
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity("Shapley values")
+        return c
 
     for _ in range(args.warmup):
-        step()
+        one_step()
     barrier(world)
-    # kernel-only timing with HIP events on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    timer = KernelTimer(args.profile_kernel)
+    eng.profiler = timer
+    reps0 = eng.stats["replicas"]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        agg.partial(V, begin)
-        ev[i][1].record(stream)
-        if world > 1:
-            dist.all_reduce(agg.partial_buf)
-        agg.finalize(agg.partial_buf)
+    for _ in range(args.steps):
+        c = one_step()
     barrier(world)
-    wall = time.perf_counter() - t0
-    wall = max_over_ranks(wall, world)
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    kern_ms = max_over_ranks(kern_ms, world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    eng.profiler = None
+    kern_ms = timer.total_ms()
+    launches = timer.launches()
+    # algorithmic work of the profiled kernel on THIS rank: every replica sees its n_p rows once per epoch
+    local_reps = eng.stats["replicas"] - reps0
+    sizes = eng.partner_sizes
+    # exact per-rank sample count: sum over this rank's replicas of E * n_p (shard is LPT over coalitions)
+    from mplc.parallel import lpt_shard, coalition_cost
+    from itertools import combinations
+    coals = [cc for r in range(1, n + 1) for cc in combinations(range(n), r)]
+    shards = lpt_shard([coalition_cost(cc, sizes) for cc in coals], world)
+    mine = [coals[i] for i in shards[rank]]
+    samples = args.steps * args.epochs * sum(sizes[p] for cc in mine for p in cc)
+    flops = samples * CONV_BWD_DATA_FLOP_PER_SAMPLE
+    achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
     ms_per_step = wall * 1000 / args.steps
-    total_bytes = (1 << n) * 8
-    value = total_bytes / (ms_per_step / 1000) / 1e9
-    shard_bytes = (end - begin) * 8
-    achieved = shard_bytes / (kern_ms / 1000) / 1e9
+    total_train_samples = sum_over_ranks(samples, world)
     out = {
-        "metric": "exact-Shapley aggregation GB/s at N=%d" % n,
-        "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": "Synthetic v(S) table, N=%d partners (2^%d fp64), range-sharded + RCCL all-reduce" % (n, n),
-                   "n": n, "table_bytes": total_bytes, "parallelism": "range-shard x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "shapley_block_kernel+reduce", "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_launch": shard_bytes},
+        "metric": "coalition v(S) evals/sec (MNIST FedAvg)",
+        "value": round(n_coal * args.steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 1), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (MNIST-shaped: x~U[0,1) fp32 [60000,28,28,1], random one-hot labels)",
+        "config": {"workload": f"BASELINE config #3: MNIST CNN, {n} partners random split, FedAvg, exact Shapley "
+                               f"over all {n_coal} coalitions (E={args.epochs} fixed, M={args.minibatches}, "
+                               f"G={args.gupp}), coalitions LPT-sharded x{world}",
+                   "partners": n, "coalitions": n_coal, "epochs": args.epochs, "minibatch_count": args.minibatches,
+                   "gradient_updates_per_pass": args.gupp, "batch_size": [int(p.batch_size) for p in sc.partners_list],
+                   "replicas_trained_per_step": int(sum_over_ranks(local_reps, world) / max(1, args.steps)),
+                   "train_samples_per_step": int(total_train_samples / args.steps),
+                   "parallelism": f"coalition-shard x{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": f"{args.profile_kernel}_kernel", "launches": launches,
+                     "kernel_ms_avg": round(kern_ms / max(1, launches), 4),
+                     "algorithmic_flop_per_launch": int(flops / max(1, launches)),
+                     "flop_per_sample": CONV_BWD_DATA_FLOP_PER_SAMPLE},
+        "shapley_values": [round(float(v), 6) for v in c.contributivity_scores],
     }
-    return out
+    return out, sc
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--leg", default="shapley", choices=["shapley"])
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--leg", default="train", choices=["train", "shapley"])
+    ap.add_argument("--partners", type=int, default=10)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--minibatches", type=int, default=20)
+    ap.add_argument("--gupp", type=int, default=8)
     ap.add_argument("--n", type=int, default=28)
+    ap.add_argument("--profile-kernel", default="conv_bwd_data")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shapley-agg", action="store_true")
     args = ap.parse_args()
     rank, world, _ = dist_init()
-    out = bench_shapley(args, rank, world)
+    if args.leg == "shapley":
+        out = bench_shapley(args.n, max(args.steps, 5), max(args.warmup, 2), rank, world)
+        out.update({"n_gpus": world, "steps": max(args.steps, 5), "warmup": max(args.warmup, 2),
+                    "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                    "data": "synthetic", "config": {"workload": f"Synthetic v(S) table N={args.n} (2^{args.n} fp64), "
+                                                                f"range-sharded + RCCL all-reduce x{world}"}})
+        if rank == 0:
+            out["cpu_baseline"] = cpu_baseline_shapley() if (world == 1 and not args.no_cpu_baseline) else None
+    else:
+        out, sc = bench_train(args, rank, world)
+        if not args.no_shapley_agg:
+            agg = bench_shapley(args.n, 10, 2, rank, world)
+            out["shapley_agg"] = agg
+        if rank == 0:
+            out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
+                                   if (world == 1 and not args.no_cpu_baseline) else None)
     if rank == 0:
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_shapley()
-        else:
-            out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -842,6 +842,11 @@ int mplc_cnn_copy_rows(float* dst, const float* src, int64_t stride, const int32
   return launch_status();
 }
 
+#define PROF_BEGIN(k) \
+  if (t->prof_kernel == (k) && t->prof_begin) (void)hipEventRecord((hipEvent_t)t->prof_begin, s)
+#define PROF_END(k) \
+  if (t->prof_kernel == (k) && t->prof_end) (void)hipEventRecord((hipEvent_t)t->prof_end, s)
+
 int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   if (!t || t->n_rep < 1 || t->n_rep > 65535 || t->bmax < 1) return MPLC_E_ARG;
   if (t->w2_splits != (t->bmax + WG_SAMPLES - 1) / WG_SAMPLES) return MPLC_E_SHAPE;
@@ -857,23 +862,37 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t);
+  PROF_BEGIN(1);
   conv_fwd_kernel<<<dim3(2, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->pooled,
                                                          t->code);
+  PROF_END(1);
+  PROF_BEGIN(2);
   dense_fwd_kernel<<<dim3((B + 31) / 32, R), 256, 0, s>>>(t->pooled, (int64_t)B * FEAT, t->cnt, 0, B, t->params, S,
                                                           t->hidden);
+  PROF_END(2);
+  PROF_BEGIN(3);
   head_kernel<<<R, 256, 0, s>>>(t->hidden, t->idx, t->labels, t->cnt, t->adam_t, B, t->params, t->adam_m, t->adam_v,
                                 S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps);
+  PROF_END(3);
+  PROF_BEGIN(4);
   dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                   t->params, t->adam_m, t->adam_v, S, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
+  PROF_END(4);
   transpose_w2_kernel<<<dim3(18, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
+  PROF_BEGIN(5);
   conv_bwd_data_kernel<<<dim3(B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
                                                           t->code, t->w1_part);
+  PROF_END(5);
+  PROF_BEGIN(6);
   conv_wgrad_kernel<<<dim3(t->w2_splits, R), WG_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->w2_splits, t->params,
                                                                  S, t->dpooled, t->code, t->w2_part);
+  PROF_END(6);
+  PROF_BEGIN(7);
   adam_small_kernel<<<dim3((OFF_W3 + 255) / 256, R), 256, 0, s>>>(t->cnt, t->adam_t, B, t->w2_splits, t->w1_part,
                                                                  t->w2_part, t->params, t->adam_m, t->adam_v, S,
                                                                  t->lr, t->beta1, t->beta2, t->eps);
+  PROF_END(7);
   return launch_status();
 }
 

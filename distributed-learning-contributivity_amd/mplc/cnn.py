@@ -58,7 +58,11 @@ class TrainT(ctypes.Structure):
                 ("dhidden", ctypes.c_void_p), ("dpooled", ctypes.c_void_p), ("w1_part", ctypes.c_void_p),
                 ("w2_part", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
-                ("eps", ctypes.c_float)]
+                ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("pad1", ctypes.c_int32),
+                ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p)]
+
+KERNEL_IDS = {"conv_fwd": 1, "dense_fwd": 2, "head": 3, "dense1_bwd_adam": 4, "conv_bwd_data": 5, "conv_wgrad": 6,
+              "adam_small": 7}
 
 
 _BOUND = False
@@ -215,6 +219,11 @@ class TrainBatch:
 
     def step(self, s):
         self.t.step = s
+        prof = self.eng.profiler
+        if prof is not None:
+            ev0, ev1 = prof.pair()
+            self.t.prof_kernel = KERNEL_IDS[prof.kernel]
+            self.t.prof_begin, self.t.prof_end = ev0, ev1
         _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(self.t), self.stream), "mplc_cnn_train_step")
 
     def aggregate(self):

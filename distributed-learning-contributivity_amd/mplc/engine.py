@@ -72,6 +72,7 @@ class CoalitionEngine:
             memory_budget_bytes = int(free * 0.8) - self.eval_budget_bytes
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
+        self.profiler = None  # optional KernelTimer (bench.py): HIP events around one kernel per step
         self.stats = {"coalitions": 0, "batches": 0, "replicas": 0}
 
     # --------------------------------------------------------------------------------------------

@@ -77,8 +77,11 @@ class MultiPartnerLearning:
 
     @classmethod
     def evaluate_coalitions(cls, scenario, coalitions):
-        """Batched v(S) for many coalitions (test accuracy of the trained coalition model), float64 array."""
-        return _engine(scenario).evaluate(list(coalitions))
+        """Batched v(S) for many coalitions (test accuracy of the trained coalition model), float64 array.
+        Under torch.distributed the coalitions are LPT-sharded over the ranks (mplc.parallel)."""
+        from .parallel import sharded_evaluate
+        eng = _engine(scenario)
+        return sharded_evaluate(eng.evaluate, list(coalitions), eng.partner_sizes, eng.device)
 
 
 class SinglePartnerLearning(MultiPartnerLearning):

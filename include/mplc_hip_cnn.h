@@ -99,6 +99,13 @@ typedef struct {
   float* w2t;             /* [n_rep][9*64*32] W2 transposed for the data-gradient MFMA    */
   /* optimizer (Keras 2.3.1 Adam) */
   float lr, beta1, beta2, eps;
+  /* optional in-stream timing of one kernel of the step (bench roofline): hipEvent_t recorded right
+   * before / after launch number prof_kernel (1 conv_fwd, 2 dense_fwd, 3 head, 4 dense1_bwd_adam,
+   * 5 conv_bwd_data, 6 conv_wgrad, 7 adam_small); 0 or NULL events = off */
+  int32_t prof_kernel;
+  int32_t pad1;
+  void* prof_begin;
+  void* prof_end;
 } mplc_cnn_train_t;
 
 /* Parameter row stride in floats (== MPLC_CNN_STRIDE). */

@@ -151,8 +151,12 @@ def forward(p, x):
     return h @ p["W4"] + p["b4"]
 
 
-def gradients(p, x, y):
+def gradients(p, x, y, dtype=None):
+    """Autograd gradients of the batch-mean CE; dtype=torch.float64 gives the high-precision reference."""
     torch = _torch()
+    if dtype is not None:
+        p = {k: v.to(dtype) for k, v in p.items()}
+        x = x.to(dtype)
     q = {k: v.clone().requires_grad_(True) for k, v in p.items()}
     logits = forward(q, x)
     loss = torch.nn.functional.cross_entropy(logits, y)  # mean over batch, from logits

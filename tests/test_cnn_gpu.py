@@ -100,14 +100,19 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
         P = ocnn.unpack(p0[r])
         x = odata.x_train[rws]
         y = odata.y_train[rws]
-        grads, _ = ocnn.gradients(P, x, y)
+        g32, _ = ocnn.gradients(P, x, y)
+        g64, _ = ocnn.gradients(P, x, y, dtype=torch.float64)
         g_dev = m[r] / np.float32(0.1)
         for name, (off, shape) in ocnn.OFF.items():
             n = int(np.prod(shape))
-            gd = g_dev[off:off + n]
-            gr = grads[name].numpy().reshape(-1)
-            err = np.linalg.norm(gd - gr) / max(np.linalg.norm(gr), 1e-12)
-            assert err < 2e-4, (r, name, err)
+            gd = g_dev[off:off + n].astype(np.float64)
+            ref = g64[name].numpy().reshape(-1)
+            scale = max(np.linalg.norm(ref), 1e-12)
+            err_dev = np.linalg.norm(gd - ref) / scale
+            err_cpu = np.linalg.norm(g32[name].numpy().reshape(-1) - ref) / scale
+            # device fp32 error vs the fp64 reference: at most a few times the CPU fp32 error (both are fp32
+            # sums in different orders; ReLU-boundary flips dominate the long conv1 reductions)
+            assert err_dev < max(4 * err_cpu, 1e-5), (r, name, err_dev, err_cpu)
         # activations
         F = torch.nn.functional
         with torch.no_grad():
