@@ -540,21 +540,30 @@ __global__ void transpose_w2_kernel(const float* __restrict__ params, int64_t st
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv2 data gradient + conv1 backward.  Block = one sample (4 waves, 22 row tiles of 32 positions).
-// dZ2[oy][ox][co] = dp[py][px][co] if the window's argmax is (oy,ox) and its max was > 0, else 0.
+// conv2 data gradient + conv1 backward.  Block = (sample, band of 13 conv1 rows), 4 waves.
+// dA1[pos][ci] = sum_{ky,kx,co} dZ2[pos-(ky,kx)][co] W2[ky][kx][ci][co]  (implicit GEMM, K = 9 x 64)
+// dZ2 (the max-pool gradient, 3/4 zeros) is un-pooled ONCE per band and channel half into a dense LDS
+// tile [15 rows][24 cols][33], so the MFMA loop reads its A operand with one ds_read + one select (column
+// bound); B (W2 transposed, [kyx][co][ci]) streams from L2.  Epilogue: ReLU' of the recomputed conv1
+// output, then conv1's weight gradient partial sums per (sample, band).
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_THREADS = 256;
+constexpr int BAND = 13;               // conv1 rows per block (2 bands cover 26 rows)
+constexpr int BAND_POS = BAND * A1;    // 338 positions
+constexpr int BAND_TILES = 11;         // ceil(338 / 32)
+constexpr int DZR = BAND + 2;          // dZ2 rows a band needs
+constexpr int DZP = 33;                // padded channel stride (32 channels per half)
 
 __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     const float* __restrict__ params, int64_t stride, const float* __restrict__ w2t,
     const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
-  __shared__ float dz_s[PL * PL * C2];
-  __shared__ uint8_t sel_s[PL * PL * C2];
-  __shared__ float img_s[IMG * IMG];
+  __shared__ float dz_s[DZR * Z2 * DZP];
+  __shared__ float img_s[(BAND + 2) * IMG];
   __shared__ float w1_s[9 * C1 + C1];
   __shared__ float red_s[4][10 * 32];
-  const int j = blockIdx.x;
+  const int band = blockIdx.x & 1;
+  const int j = blockIdx.x >> 1;
   const int r = blockIdx.y;
   if (j >= cnt[r]) return;
   const int tid = threadIdx.x;
@@ -562,50 +571,84 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
   const float* P = params + (int64_t)r * stride;
   const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
   const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
-  for (int e = tid; e < FEAT; e += BWD_THREADS) {
-    const uint8_t c = cd[e];
-    const bool pos = (c & 0x80) != 0;
-    dz_s[e] = pos ? dp[e] : 0.0f;
-    sel_s[e] = pos ? (c & 3) : 4;
-  }
-  for (int e = tid; e < IMG * IMG; e += BWD_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + e];
+  const int iy0 = band * BAND;
+  const int oy0 = iy0 - 2;  // dZ2 row of local row 0
+  for (int e = tid; e < (BAND + 2) * IMG; e += BWD_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + iy0 * IMG + e];
   for (int e = tid; e < 9 * C1 + C1; e += BWD_THREADS) w1_s[e] = P[OFF_W1 + e];
-  __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31;
   const int kh = lane >> 5;
   const float* T = w2t + (int64_t)r * (9 * C1 * C2);
+  // this wave's tiles: wave, wave+4, wave+8 (wave 3: two tiles)
+  const int ntile = (wave + 8 < BAND_TILES) ? 3 : 2;
+  floatx16 acc[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) acc[u] = zero16();
+  int iyl[3], ixx[3];
+  bool valid[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int pl = (wave + 4 * u) * 32 + n;
+    valid[u] = (u < ntile) && (pl < BAND_POS);
+    iyl[u] = pl / A1;  // local conv1 row (0..12)
+    ixx[u] = pl % A1;
+  }
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // previous half's readers are done
+    for (int e = tid; e < DZR * Z2 * 32; e += BWD_THREADS) {
+      const int c = e & 31;
+      const int px = (e >> 5) % Z2;
+      const int lr = e / (32 * Z2);
+      const int oy = oy0 + lr;
+      float v = 0.0f;
+      if (oy >= 0 && oy < Z2) {
+        const int pidx = ((oy >> 1) * PL + (px >> 1)) * C2 + half * 32 + c;
+        const uint8_t cc = cd[pidx];
+        const int q = (oy & 1) * 2 + (px & 1);
+        if ((cc & 0x80) && (cc & 3) == q) v = dp[pidx];
+      }
+      dz_s[(lr * Z2 + px) * DZP + c] = v;
+    }
+    __syncthreads();
+    for (int kyx = 0; kyx < 9; ++kyx) {
+      const int ky = kyx / 3, kx = kyx % 3;
+      int base[3];
+      bool inb[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int ox = ixx[u] - kx;
+        inb[u] = valid[u] && ox >= 0 && ox < Z2;
+        // dZ2 local row = (iy0 + iyl - ky) - oy0 = iyl - ky + 2  (0..14)
+        base[u] = inb[u] ? ((iyl[u] - ky + 2) * Z2 + ox) * DZP : 0;
+      }
+      const float* Tk = T + (kyx * C2 + half * 32) * C1 + n;
+#pragma unroll 8
+      for (int c2 = 0; c2 < 16; ++c2) {
+        const int c = 2 * c2 + kh;
+        const float b = Tk[c * C1];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const float a = inb[u] ? dz_s[base[u] + c] : 0.0f;
+          acc[u] = mfma32(a, b, acc[u]);
+        }
+      }
+    }
+  }
+  // epilogue: ReLU' of the recomputed conv1 output, conv1 weight gradient
   float gw1[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) gw1[i] = 0.0f;
   float gb1 = 0.0f;
-  // tiles t = wave, wave+4, ...  (22 tiles of 32 positions over 676)
-  for (int t = wave; t < 22; t += 4) {
-    const int mpos = t * 32 + n;  // A row of this lane
-    const int iy = mpos / A1, ix = mpos % A1;
-    floatx16 acc = zero16();
-    for (int kyx = 0; kyx < 9; ++kyx) {
-      const int ky = kyx / 3, kx = kyx % 3;
-      const int oy = iy - ky, ox = ix - kx;
-      const bool inb = (mpos < A1 * A1) && oy >= 0 && oy < Z2 && ox >= 0 && ox < Z2;
-      const int cell = inb ? ((oy >> 1) * PL + (ox >> 1)) * C2 : 0;
-      const int q = inb ? ((oy & 1) * 2 + (ox & 1)) : 5;
-      const float* Tk = T + kyx * C2 * C1 + n;
-#pragma unroll 8
-      for (int c2 = 0; c2 < 32; ++c2) {
-        const int co = 2 * c2 + kh;
-        const float a = (sel_s[cell + co] == q) ? dz_s[cell + co] : 0.0f;
-        const float b = Tk[co * C1];
-        acc = mfma32(a, b, acc);
-      }
-    }
-    // epilogue: ReLU' of recomputed conv1 output, conv1 weight gradient
+  const int ci = n;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    if (u >= ntile) break;
+    const int t = wave + 4 * u;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int prow = t * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
-      if (prow < A1 * A1) {
-        const int py = prow / A1, px = prow % A1;
-        const int ci = n;
+      const int pl = t * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+      if (pl < BAND_POS) {
+        const int py = pl / A1, px = pl % A1;  // local row py (image rows py..py+2 in img_s)
         float a1 = w1_s[9 * C1 + ci];
         float pix[9];
 #pragma unroll
@@ -614,7 +657,7 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
           a1 += pix[k] * w1_s[k * C1 + ci];
         }
         if (a1 > 0.0f) {
-          const float dz = acc[reg];
+          const float dz = acc[u][reg];
 #pragma unroll
           for (int k = 0; k < 9; ++k) gw1[k] += pix[k] * dz;
           gb1 += dz;
@@ -622,7 +665,6 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
       }
     }
   }
-  // reduce over lane halves (same ci) and waves
 #pragma unroll
   for (int k = 0; k < 9; ++k) gw1[k] += __shfl_xor(gw1[k], 32, 64);
   gb1 += __shfl_xor(gb1, 32, 64);
@@ -632,7 +674,7 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
     red_s[wave][9 * 32 + n] = gb1;
   }
   __syncthreads();
-  float* out = w1_part + ((int64_t)r * bmax + j) * MPLC_CNN_W1P;
+  float* out = w1_part + (((int64_t)r * bmax + j) * 2 + band) * MPLC_CNN_W1P;
   for (int e = tid; e < 10 * 32; e += BWD_THREADS)
     out[e] = (red_s[0][e] + red_s[1][e]) + (red_s[2][e] + red_s[3][e]);
 }
@@ -644,6 +686,7 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_THREADS = 192;
 constexpr int WG_SAMPLES = 8;  // samples per wgrad split (fixed: reproducible sums)
+constexpr int WGP = 65;        // padded channel stride of the dense dZ2 band
 
 __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
@@ -652,9 +695,7 @@ __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
   __shared__ float img_s[IMG * IMG];
   __shared__ float w1_s[9 * C1 + C1];
   __shared__ float a1_s[6 * A1 * C1];
-  __shared__ float dz_s[2 * PL * C2];
-  __shared__ uint8_t sel_s[2 * PL * C2];
-  __shared__ float red_s[3][2][32];
+  __shared__ float dzd_s[4 * Z2 * WGP];  // dense un-pooled dZ2 of the band: [4 rows][24 cols][65]
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -691,12 +732,15 @@ __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
         for (int k = 0; k < 9; ++k) a += img_s[(gy + k / 3) * IMG + lc + k % 3] * w1_s[k * C1 + ci];
         a1_s[e] = fmaxf(a, 0.0f);
       }
-      for (int e = tid; e < 2 * PL * C2; e += WG_THREADS) {
-        const int ge = band * 2 * PL * C2 + e;
-        const uint8_t c = cd[ge];
-        const bool pos = (c & 0x80) != 0;
-        dz_s[e] = pos ? dp[ge] : 0.0f;
-        sel_s[e] = pos ? (c & 3) : 4;
+      for (int e = tid; e < 4 * Z2 * C2; e += WG_THREADS) {
+        const int co = e & 63;
+        const int px = (e >> 6) % Z2;
+        const int oyl = e / (64 * Z2);
+        const int oy = 4 * band + oyl;
+        const int pidx = ((oy >> 1) * PL + (px >> 1)) * C2 + co;
+        const uint8_t c = cd[pidx];
+        const int q = (oy & 1) * 2 + (px & 1);
+        dzd_s[(oyl * Z2 + px) * WGP + co] = ((c & 0x80) && (c & 3) == q) ? dp[pidx] : 0.0f;
       }
       __syncthreads();
       // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh)
@@ -704,10 +748,8 @@ __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
       for (int s = 0; s < 48; ++s) {
         const int px = 2 * s + kh;          // 0..95 within band
         const int oyl = px / Z2, ox = px % Z2;  // oyl 0..3
-        const int cell = ((oyl >> 1) * PL + (ox >> 1)) * C2;
-        const int q = (oyl & 1) * 2 + (ox & 1);
-        const float bz0 = (sel_s[cell + m] == q) ? dz_s[cell + m] : 0.0f;
-        const float bz1 = (sel_s[cell + 32 + m] == q) ? dz_s[cell + 32 + m] : 0.0f;
+        const float bz0 = dzd_s[(oyl * Z2 + ox) * WGP + m];
+        const float bz1 = dzd_s[(oyl * Z2 + ox) * WGP + 32 + m];
         if (wave == 0) { gb[0] += bz0; gb[1] += bz1; }
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
@@ -755,8 +797,8 @@ __global__ void adam_small_kernel(const int32_t* __restrict__ cnt, const int32_t
   if (e >= OFF_W3) return;
   float g = 0.0f;
   if (e < OFF_W2) {
-    const float* w = w1_part + (int64_t)r * bmax * MPLC_CNN_W1P + e;
-    for (int jj = 0; jj < count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];
+    const float* w = w1_part + (int64_t)r * bmax * 2 * MPLC_CNN_W1P + e;
+    for (int jj = 0; jj < 2 * count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];  // (sample, band) order
   } else {
     const float* w = w2_part + (int64_t)r * splits * MPLC_CNN_W2P + (e - OFF_W2);
     const int used = (count + WG_SAMPLES - 1) / WG_SAMPLES;
@@ -881,7 +923,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   PROF_END(4);
   transpose_w2_kernel<<<dim3(18, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(5);
-  conv_bwd_data_kernel<<<dim3(B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
+  conv_bwd_data_kernel<<<dim3(2 * B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
                                                           t->code, t->w1_part);
   PROF_END(5);
   PROF_BEGIN(6);

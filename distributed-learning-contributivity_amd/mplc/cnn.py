@@ -173,7 +173,7 @@ class TrainBatch:
             idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
             pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
             hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
-            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, W1P), **f32),
+            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, 2, W1P), **f32),
             w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, 9 * 64 * 32), **f32))
         t = TrainT()
         t.n_rep, t.bmax, t.w2_splits = R, B, splits

@@ -131,14 +131,19 @@ class ArrayDataset(Dataset):
     train_val_split_local = staticmethod(Mnist.train_val_split_local)
 
 
-def digits_as_mnist(seed=0):
-    """sklearn's bundled 8x8 digits (no network) upsampled x3 and padded to 28x28, values / 16:
-    a small real, learnable MNIST-shaped dataset for accuracy tests.  Returns (x, y_onehot)."""
+def digits_as_mnist(seed=0, noise=0.02):
+    """sklearn's bundled 8x8 digits (no network) upsampled x3 and padded to 28x28, values / 16, plus a
+    little seeded uniform noise: a small real, learnable MNIST-shaped dataset for accuracy tests.  The noise
+    breaks the exact pixel symmetries of the block upsampling (which would create exact max-pool ties whose
+    winner then depends on the last bit of each implementation's conv sums).  Returns (x, y_onehot)."""
     from sklearn.datasets import load_digits
     d = load_digits()
     x = d.images.astype(np.float32) / 16.0
     x = np.kron(x, np.ones((3, 3), dtype=np.float32))
     x = np.pad(x, ((0, 0), (2, 2), (2, 2)))[..., None]
+    if noise:
+        x = (x * (1 - noise) + noise * np.random.default_rng(seed).random(x.shape, dtype=np.float32))
+        x = x.astype(np.float32)
     y = _one_hot(d.target, 10)
     return x, y
 

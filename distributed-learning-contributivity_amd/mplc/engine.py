@@ -98,7 +98,7 @@ class CoalitionEngine:
 
     # --------------------------------------------------------------------------------------------
     def replica_bytes(self, bmax):
-        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + bmax * W1P * 4 + 4 * W2P * 4
+        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + 2 * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
                 + 9 * 64 * 32 * 4 + bmax * 12)
 
     def plan_batches(self, coalitions):

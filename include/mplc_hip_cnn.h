@@ -94,7 +94,7 @@ typedef struct {
   float* hidden;          /* [n_rep][bmax][128]                                           */
   float* dhidden;         /* [n_rep][bmax][128]                                           */
   float* dpooled;         /* [n_rep][bmax][9216]                                          */
-  float* w1_part;         /* [n_rep][bmax][MPLC_CNN_W1P]                                  */
+  float* w1_part;         /* [n_rep][bmax][2][MPLC_CNN_W1P] (per sample and row band)     */
   float* w2_part;         /* [n_rep][w2_splits][MPLC_CNN_W2P]                             */
   float* w2t;             /* [n_rep][9*64*32] W2 transposed for the data-gradient MFMA    */
   /* optimizer (Keras 2.3.1 Adam) */

@@ -164,6 +164,29 @@ def gradients(p, x, y, dtype=None):
     return {k: v.grad.detach() for k, v in q.items()}, float(loss.detach())
 
 
+def conv1_relu_flip_bound(p, x, y, rel_tau=1e-6):
+    """Upper bound on how much the W1 / b1 gradients can move if the ReLU mask of conv1 flips at positions
+    whose pre-activation is within rel_tau * max|a1| of zero (fp32 recomputations in a different summation
+    order may land on either side): |pix| * |dL/da1| summed over those positions, in fp64."""
+    torch = _torch()
+    F = torch.nn.functional
+    p = {k: v.to(torch.float64) for k, v in p.items()}
+    x = x.to(torch.float64)
+    z1 = F.conv2d(x.unsqueeze(1), p["W1"].permute(3, 2, 0, 1), p["b1"])
+    a1 = F.relu(z1).detach().requires_grad_(True)
+    h = F.max_pool2d(F.relu(F.conv2d(a1, p["W2"].permute(3, 2, 0, 1), p["b2"])), 2)
+    h = F.relu(h.permute(0, 2, 3, 1).reshape(h.shape[0], -1) @ p["W3"] + p["b3"])
+    loss = F.cross_entropy(h @ p["W4"] + p["b4"], y)
+    loss.backward()
+    da1 = a1.grad.abs()                                   # [b, 32, 26, 26]
+    az = z1.detach().abs()
+    near = ((az > 0) & (az <= rel_tau * az.max())).to(torch.float64)  # exact zeros agree on both sides
+    w = da1 * near
+    patches = F.unfold(x.unsqueeze(1).abs(), 3)           # [b, 9, 676]
+    bw = torch.einsum("bkp,bcp->kc", patches, w.reshape(w.shape[0], 32, -1))
+    return bw.reshape(-1).numpy(), w.sum(dim=(0, 2, 3)).numpy()
+
+
 class KerasAdam:
     """Keras 2.3.1 Adam (keras/optimizers.py get_updates), float32."""
 

@@ -6,6 +6,5 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.lo
 rc=$?
 echo "pytest rc $rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then echo "stop after pytest rc $rc"; exit $rc; fi
-timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- python bench.py --no-cpu-baseline --no-shapley-agg > gpurun_out/prof_bench.log 2>&1
+timeout -k 10 600 python scripts/probe_scale.py 512 5 400 12 > gpurun_out/probe_scale.log 2>&1
 echo EXIT $?

@@ -95,6 +95,7 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
     pooled = st.ws["pooled"].cpu().numpy()
     hidden = st.ws["hidden"].cpu().numpy()
     assert np.array_equal(st.params.cpu().numpy(), p0)  # lr = 0: no update
+    report, bad = [], []
     for r in range(st.R):
         rws = idx[r, :cnt[r]]
         P = ocnn.unpack(p0[r])
@@ -102,6 +103,7 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
         y = odata.y_train[rws]
         g32, _ = ocnn.gradients(P, x, y)
         g64, _ = ocnn.gradients(P, x, y, dtype=torch.float64)
+        flip = ocnn.conv1_relu_flip_bound(P, x, y)
         g_dev = m[r] / np.float32(0.1)
         for name, (off, shape) in ocnn.OFF.items():
             n = int(np.prod(shape))
@@ -111,8 +113,14 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
             err_dev = np.linalg.norm(gd - ref) / scale
             err_cpu = np.linalg.norm(g32[name].numpy().reshape(-1) - ref) / scale
             # device fp32 error vs the fp64 reference: at most a few times the CPU fp32 error (both are fp32
-            # sums in different orders; ReLU-boundary flips dominate the long conv1 reductions)
-            assert err_dev < max(4 * err_cpu, 1e-5), (r, name, err_dev, err_cpu)
+            # sums in different orders).  conv1's gradients may additionally move by the contribution of
+            # positions whose pre-activation is ~0 (ReLU mask decided by rounding): bounded explicitly.
+            allow = max(4 * err_cpu, 1e-5)
+            if name in ("W1", "b1"):
+                allow += np.linalg.norm(flip[0] if name == "W1" else flip[1]) / scale
+            report.append((r, name, float(err_dev), float(err_cpu), float(allow)))
+            if not err_dev < allow:
+                bad.append(report[-1])
         # activations
         F = torch.nn.functional
         with torch.no_grad():
@@ -122,6 +130,7 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
             hid = np.maximum(flat @ P["W3"].numpy() + P["b3"].numpy(), 0)
         assert np.max(np.abs(pooled[r, :cnt[r]] - flat)) <= 1e-4 * max(1.0, np.max(np.abs(flat)))
         assert np.max(np.abs(hidden[r, :cnt[r]] - hid)) <= 1e-4 * max(1.0, np.max(np.abs(hid)))
+    assert not bad, (bad, report)
 
 
 def test_one_adam_step_matches_keras_adam(scenario, engine, odata):
