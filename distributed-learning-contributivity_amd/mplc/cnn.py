@@ -282,7 +282,10 @@ class CnnBatchTrainer:
         spe = {ci: -(-sizes[coalitions[ci][0]] // eng.batch_sizes[coalitions[ci][0]])
                for ci in range(C) if st.coal_is_single[ci]}
         per_epoch_fed = eng.minibatch_count * st.round_len
+        progress = getattr(eng, "progress", None)
         for s in range(st.total_steps):
+            if progress is not None and s % 30 == 0:
+                progress(s, st.total_steps, st.R)
             if use_es and st.fed_steps and s % per_epoch_fed == 0 and s < st.fed_steps:
                 live = [ci for ci in fed if not st.stopped[ci]]
                 if live:  # val loss of each live global model at the start of epoch e (minibatch 0)

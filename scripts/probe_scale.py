@@ -30,11 +30,18 @@ def main():
     coals = sorted(coals)
     for b in budgets:
         eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=int(b * (1 << 30)))
+        t_start = [time.time()]
+
+        def progress(s, total, R):
+            torch.cuda.synchronize()
+            print(f"    step {s}/{total} R={R} t={time.time() - t_start[0]:.2f}s", flush=True)
+        eng.progress = progress
         eng.evaluate(coals[:2])
         for kern in ("conv_bwd_data", "dense1_bwd_adam"):
             eng.profiler = KernelTimer(kern)
             torch.cuda.synchronize()
             t0 = time.time()
+            t_start[0] = t0
             eng.evaluate(coals)
             torch.cuda.synchronize()
             dt = time.time() - t0
