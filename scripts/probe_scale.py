@@ -1,5 +1,5 @@
 """Probe: per-replica-step cost vs lockstep batch size (HBM budget), config #3 shape, E=1.
-python scripts/probe_scale.py n_coalitions size budget_gb [budget_gb ...]"""
+python scripts/probe_scale.py n_coalitions size(0 = any size >= 2) budget_gb [budget_gb ...]"""
 import os
 import sys
 import time
@@ -23,11 +23,13 @@ def main():
     budgets = [float(b) for b in sys.argv[3:]] or [400]
     sc = Scenario(10, [0.1] * 10, dataset=Mnist(synthetic=True), minibatch_count=20, epoch_count=1,
                   is_early_stopping=False).provision()
+    from itertools import combinations
+    pool = [c for r in range(2, 11) for c in combinations(range(10), r)] if size == 0 else \
+        list(combinations(range(10), size))
     rng = np.random.default_rng(0)
-    coals = set()
-    while len(coals) < n:
-        coals.add(tuple(sorted(rng.choice(10, size=size, replace=False).tolist())))
-    coals = sorted(coals)
+    pick = rng.choice(len(pool), size=min(n, len(pool)), replace=False)
+    coals = sorted(pool[i] for i in pick)
+    n = len(coals)
     for b in budgets:
         eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=int(b * (1 << 30)))
         t_start = [time.time()]
@@ -47,7 +49,7 @@ def main():
             dt = time.time() - t0
             ms = eng.profiler.total_ms()
             nb = len(eng.plan_batches(coals))
-            reps = n * size
+            reps = sum(len(c) for c in coals)
             print(f"budget {b:6.1f} GB: {nb} batches, {reps} replicas: {dt:6.2f}s total, {kern} {ms:8.1f} ms "
                   f"({ms * 1000 / (reps * 180):.2f} us per replica-step)", flush=True)
         del eng

@@ -23,11 +23,11 @@ def main():
     sc = Scenario(10, [0.1] * 10, dataset=Mnist(synthetic=True), minibatch_count=20, epoch_count=E,
                   is_early_stopping=False).provision()
     eng = CoalitionEngine.for_scenario(sc)
+    from itertools import combinations
+    pool = list(combinations(range(10), size))
     rng = np.random.default_rng(0)
-    coals = set()
-    while len(coals) < n:
-        coals.add(tuple(sorted(rng.choice(10, size=size, replace=False).tolist())))
-    coals = sorted(coals)
+    coals = sorted(pool[i] for i in rng.choice(len(pool), size=min(n, len(pool)), replace=False))
+    n = len(coals)
     t0 = time.time()
     eng.evaluate(coals[:2])
     torch.cuda.synchronize()
