@@ -30,6 +30,10 @@ SIGNATURES = {
     "mplc_cnn_train_step": (c_int, [c_void_p, c_void_p]),
     "mplc_cnn_evaluate": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),
+    # batched FedAvg logistic regression (Titanic)
+    "mplc_lr_fedavg": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 ABI_VERSION = 1

@@ -120,6 +120,60 @@ class Mnist(Dataset):
         return train_test_split(x, y, test_size=0.1, random_state=42)
 
 
+class Titanic(Dataset):
+    """mplc/dataset.py:212-394: 27 engineered features, binary label; model = L2 logistic regression
+    (the engine's batched exact solver, mplc/lr.py).  Loads a local ``titanic.csv`` (the file the reference
+    caches under mplc/local_data/titanic/) from $MPLC_DATA_DIR or ./data and applies the reference's
+    feature engineering (mplc/dataset.py:235-258, including its Sex == "Male" quirk); without it, a
+    Titanic-shaped synthetic set (make_classification(887, 27, n_informative=8, random_state=0))."""
+
+    def __init__(self, synthetic=None, x=None, y=None):
+        self.num_classes = 2
+        if x is None:
+            x, y, self.synthetic = self._load(synthetic)
+        else:
+            self.synthetic = False
+        x = np.asarray(x, dtype=np.float32)
+        y = np.asarray(y, dtype=np.float32)
+        x_train, x_test, y_train, y_test = train_test_split(x, y, test_size=0.1, random_state=42)
+        super().__init__("titanic", (x.shape[1],), 2, x_train, y_train, x_test, y_test)
+
+    @staticmethod
+    def _load(synthetic):
+        if not synthetic:
+            for d in (os.environ.get("MPLC_DATA_DIR", ""), os.path.join(os.getcwd(), "data")):
+                p = os.path.join(d, "titanic.csv") if d else ""
+                if p and os.path.exists(p):
+                    import pandas as pd
+                    raw = pd.read_csv(p)
+                    if raw.columns[0].startswith("Unnamed"):
+                        raw = raw.drop(raw.columns[0], axis=1)
+                    xdf = raw.drop("Survived", axis=1)
+                    xdf["Fam_size"] = xdf["Siblings/Spouses Aboard"] + xdf["Parents/Children Aboard"]
+                    xdf["Name_Len"] = [len(i) for i in xdf["Name"]]
+                    xdf["Is_alone"] = [i == 0 for i in xdf["Fam_size"]]
+                    xdf["Sex"] = [i == "Male" for i in xdf["Sex"]]
+                    xdf["Title"] = [i.split()[0] for i in xdf["Name"]]
+                    xdf = pd.concat([xdf, pd.get_dummies(xdf["Title"])], axis=1)
+                    xdf = pd.concat([xdf, pd.get_dummies(xdf["Pclass"])], axis=1)
+                    xdf = xdf.drop(["Name", "Pclass", "Siblings/Spouses Aboard", "Parents/Children Aboard", "Title"],
+                                   axis=1)
+                    return xdf.to_numpy(dtype="float32"), raw["Survived"].to_numpy(dtype="float32"), False
+        if synthetic is False:
+            raise FileNotFoundError("titanic.csv not found (set MPLC_DATA_DIR); no network to download it")
+        from sklearn.datasets import make_classification
+        X, y = make_classification(n_samples=887, n_features=27, n_informative=8, random_state=0)
+        return X.astype("float32"), y.astype("float32"), True
+
+    @staticmethod
+    def train_test_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+    @staticmethod
+    def train_val_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+
 class ArrayDataset(Dataset):
     """An MNIST-shaped dataset from caller arrays (tests, sklearn digits upsampled, private data).
     Uses the MNIST local splits (train_test_split 0.1, random_state 42, twice)."""
@@ -148,4 +202,4 @@ def digits_as_mnist(seed=0, noise=0.02):
     return x, y
 
 
-__all__ = ["Dataset", "Mnist", "ArrayDataset", "digits_as_mnist", "constants"]
+__all__ = ["Dataset", "Mnist", "Titanic", "ArrayDataset", "digits_as_mnist", "constants"]

@@ -78,8 +78,15 @@ class CoalitionEngine:
     # --------------------------------------------------------------------------------------------
     @classmethod
     def for_scenario(cls, scenario, **overrides):
+        """Engine for the scenario's dataset: the batched CNN for MNIST, the batched logistic regression for
+        Titanic (mplc/dataset.py:323-394)."""
         ds = scenario.dataset
         name = getattr(ds, "name", "mnist")
+        if name == "titanic" and cls is CoalitionEngine:
+            from .lr import LogRegEngine
+            target = LogRegEngine
+        else:
+            target = cls
         model = {"mnist": "mnist_cnn"}.get(name, name)
         parts = scenario.partners_list
         rows = []
@@ -94,7 +101,9 @@ class CoalitionEngine:
                   is_early_stopping=getattr(scenario, "is_early_stopping", True),
                   seed=getattr(scenario, "engine_seed", int(os.environ.get("MPLC_ENGINE_SEED", "0"))), model=model)
         kw.update(overrides)
-        return cls(**kw)
+        if target is not cls:
+            kw.pop("batch_sizes", None)
+        return target(**kw)
 
     # --------------------------------------------------------------------------------------------
     def replica_bytes(self, bmax):

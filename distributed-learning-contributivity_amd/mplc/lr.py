@@ -1,0 +1,100 @@
+"""Titanic logistic-regression coalition engine (host side of csrc/logreg.hip).
+
+All requested coalitions are trained in ONE launch (a workgroup per coalition runs its whole FedAvg:
+epochs x minibatch rounds x partner fits + aggregation + test accuracy).  See include/mplc_hip.h
+``mplc_lr_fedavg`` for the semantics and the reference lines it replaces.
+"""
+import numpy as np
+
+from . import _native
+from .cnn import minibatch_bounds, shuffle_key
+from .fedavg import aggregation_weights
+
+MAXP = 64
+
+
+class LogRegEngine:
+    def __init__(self, *, x_train, y_train, x_val, y_val, x_test, y_test, partner_rows, epoch_count, minibatch_count,
+                 aggregation="data-volume", is_early_stopping=True, seed=0, device=None, **_):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("MI355X (HIP) device required: the MPLC engine has no CPU fallback")
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.seed = int(seed)
+        self.epoch_count = int(epoch_count)
+        self.minibatch_count = int(minibatch_count)
+        self.aggregation = aggregation
+        self.is_early_stopping = bool(is_early_stopping)
+
+        def feats(x):
+            return torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float32))).to(self.device)
+
+        def labs(y):
+            y = np.asarray(y)
+            if y.ndim == 2:
+                y = np.argmax(y, axis=1)
+            return torch.from_numpy(np.ascontiguousarray(y.astype(np.float32))).to(self.device)
+
+        self.x_train_d, self.y_train_d = feats(x_train), labs(y_train)
+        self.x_val_d, self.y_val_d = feats(x_val), labs(y_val)
+        self.x_test_d, self.y_test_d = feats(x_test), labs(y_test)
+        self.n_features = int(self.x_train_d.shape[1])
+        self.partner_sizes = [int(len(r)) for r in partner_rows]
+        rows, offs, splits = [], [], []
+        for r in partner_rows:
+            offs.append(len(rows))
+            rows.extend(int(i) for i in r)
+            splits.extend(minibatch_bounds(len(r), self.minibatch_count))
+        i32 = dict(dtype=torch.int32, device=self.device)
+        self.rows_d = torch.tensor(rows, **i32)
+        self.rows_off_d = torch.tensor(offs, **i32)
+        self.n_rows_d = torch.tensor(self.partner_sizes, **i32)
+        self.splits_d = torch.tensor(splits, **i32)
+        self.stats = {"coalitions": 0, "batches": 0, "replicas": 0}
+        self.profiler = None
+        self.last_theta = None
+
+    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):
+        import torch
+        coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
+        C = len(coalitions)
+        E = self.epoch_count if epoch_count is None else int(epoch_count)
+        es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
+        masks = np.zeros(C, dtype=np.uint64)
+        keys = np.zeros((C, MAXP), dtype=np.uint64)
+        w = np.zeros((C, MAXP), dtype=np.float64)
+        scale = np.ones(C, dtype=np.float64)
+        for ci, c in enumerate(coalitions):
+            if len(c) > MAXP or c[-1] >= len(self.partner_sizes):
+                raise ValueError(f"invalid coalition {c}")
+            mask = sum(1 << p for p in c)
+            masks[ci] = mask
+            for i, p in enumerate(c):
+                keys[ci, i] = shuffle_key(self.seed, mask, p)
+            if len(c) > 1:
+                ww, scl = aggregation_weights([self.partner_sizes[p] for p in c], self.aggregation)
+                w[ci, :len(c)] = ww
+                scale[ci] = scl
+        dev = self.device
+        t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+        masks_d = t(masks.view(np.int64))
+        keys_d = t(keys.view(np.int64).reshape(-1).copy())
+        w_d, scale_d = t(w.reshape(-1).copy()), t(scale)
+        correct = torch.zeros(C, dtype=torch.int32, device=dev)
+        epochs_done = torch.zeros(C, dtype=torch.int32, device=dev)
+        theta = torch.zeros((C, self.n_features + 1), dtype=torch.float64, device=dev)
+        P = _native.ptr
+        st = _native.lib().mplc_lr_fedavg(
+            P(self.x_train_d), P(self.y_train_d), self.n_features, P(self.rows_d), P(self.rows_off_d), P(self.n_rows_d),
+            P(self.splits_d), self.minibatch_count, P(masks_d), P(keys_d), P(w_d), P(scale_d), C, E, 1 if es else 0,
+            P(self.x_val_d), P(self.y_val_d), int(self.y_val_d.numel()), P(self.x_test_d), P(self.y_test_d),
+            int(self.y_test_d.numel()), P(correct), P(epochs_done), P(theta), _native.stream_handle(dev))
+        _native.check(st, "mplc_lr_fedavg")
+        scores = correct.cpu().numpy().astype(np.float64) / float(self.y_test_d.numel())
+        self.last_theta = theta.cpu().numpy()
+        self.stats["coalitions"] += C
+        self.stats["batches"] += 1
+        self.stats["replicas"] += sum(len(c) for c in coalitions)
+        if return_details:
+            return {"scores": scores, "epochs_done": epochs_done.cpu().numpy().astype(np.int64)}
+        return scores

@@ -46,6 +46,8 @@ class Scenario:
             self.dataset = dataset
         elif dataset_name == constants.MNIST:
             self.dataset = dataset_module.Mnist()
+        elif dataset_name == constants.TITANIC:
+            self.dataset = dataset_module.Titanic()
         else:
             raise Exception(f"Dataset named '{dataset_name}' is not supported by the MI355X engine (yet)")
         self.dataset_proportion = dataset_proportion

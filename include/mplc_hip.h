@@ -82,6 +82,26 @@ int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, cons
                           int64_t out_stride, int broadcast, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Batched FedAvg logistic regression (Titanic model, BASELINE config #2), one workgroup per coalition.
+ * Replaces, per coalition, FederatedAverageLearning.fit (mplc/multi_partner_learning.py:195-216,
+ * 285-334) with the Titanic.LogisticRegression model (mplc/dataset.py:323-394: sklearn L2 LR, C=1),
+ * np.average aggregation (mplc/mpl_utils.py:90-115) and the test accuracy (:158-169).  Every fit is the
+ * exact optimum (damped Newton, fp64).  Singletons (the reference crashes there: callbacks= passed to the
+ * LR fit, mplc/multi_partner_learning.py:254-260) are one fit on the partner's full data.
+ *  x [N][n_features] fp32, y [N] fp32 0/1; rows/rows_off/n_rows: partners' row ids into x;
+ *  splits: M+1 minibatch boundaries per partner (partner p at p*(M+1)); masks[c]: coalition bitmask;
+ *  keys[c*64 + i], agg_w[c*64 + i]: shuffle key and aggregation weight of the i-th partner (ascending id)
+ *  of coalition c; agg_scale[c]: np.average's weight sum.  Outputs: correct[c] test hits,
+ *  epochs_done[c], theta_out[c][n_features+1] = [coef | intercept].  n_features <= 30.
+ * ---------------------------------------------------------------------------------------------- */
+int mplc_lr_fedavg(const float* x, const float* y, int n_features, const int32_t* rows, const int32_t* rows_off,
+                   const int32_t* n_rows, const int32_t* splits, int minibatch_count, const uint64_t* masks,
+                   const uint64_t* keys, const double* agg_w, const double* agg_scale, int n_coalitions, int epochs,
+                   int early_stopping, const float* x_val, const float* y_val, int n_val, const float* x_test,
+                   const float* y_test, int n_test, int32_t* correct, int32_t* epochs_done, double* theta_out,
+                   void* stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Batched multi-model MNIST CNN trainer (mplc/dataset.py:457-479 architecture; Keras 2.3.1 Adam).
  * One "replica" = one (coalition, partner) model.  Replaces, for B replicas at once, the per-partner
  * Keras `model.fit(x_mb, y_mb, batch_size=bs_p, epochs=1)` of mplc/multi_partner_learning.py:319-332

@@ -1,0 +1,111 @@
+"""Titanic (BASELINE config #2): batched FedAvg logistic regression.
+
+tests/golden/fedavg_lr.json holds the REFERENCE's own v(S) for 71 coalitions (3-, 5- and 10-partner
+scenarios on Titanic-shaped data, run through mplc.Scenario / FederatedAverageLearning with
+Titanic.LogisticRegression here).  The reference's sklearn lbfgs stops at tol 1e-4; the oracle and the
+device kernel solve each fit exactly, so predictions may differ from the reference only on test points
+that sit within that tolerance of the decision boundary: 2 of 71 coalitions differ by one test sample.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import lr as olr
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "fedavg_lr.json")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)["data"]
+
+
+def scenario_for(golden, case):
+    from mplc.dataset import Titanic
+    from mplc.scenario import Scenario
+    X = np.array(golden["data"]["X"], dtype=np.float32)
+    y = np.array(golden["data"]["y"], dtype=np.float32)
+    ds = Titanic(x=X, y=y)
+    sc = Scenario(case["partners_count"], case["amounts"], dataset=ds, epoch_count=case["epoch_count"],
+                  minibatch_count=case["minibatch_count"], is_early_stopping=False)
+    return sc.provision()
+
+
+def test_oracle_vs_reference_fedavg_lr(golden):
+    from sklearn.model_selection import train_test_split
+    X = np.array(golden["data"]["X"], dtype=np.float32)
+    y = np.array(golden["data"]["y"], dtype=np.float32)
+    _, xte, _, yte = train_test_split(X, y, test_size=0.1, random_state=42)
+    total, exact, worst = 0, 0, 0
+    for case in golden["cases"]:
+        parts = [(np.array(p["x_train"]), np.array(p["y_train"])) for p in case["partners"]]
+        for k, v in case["values"].items():
+            coal = tuple(int(i) for i in k.split(","))
+            mine = olr.fedavg_value(parts, coal, xte, yte)
+            total += 1
+            exact += mine == v
+            worst = max(worst, round(abs(mine - v) * len(yte)))
+    assert total == 71
+    assert exact >= 69 and worst <= 1
+
+
+def test_titanic_scenario_partitions_match_reference(golden):
+    for case in golden["cases"]:
+        sc = scenario_for(golden, case)
+        for p, gp in zip(sc.partners_list, case["partners"]):
+            assert np.array_equal(p.x_train, np.array(gp["x_train"], dtype=np.float32))
+            assert np.array_equal(p.y_train, np.array(gp["y_train"], dtype=np.float32))
+            assert p.batch_size == gp["batch_size"]
+
+
+@pytest.mark.gpu
+def test_device_lr_fedavg_matches_oracle_and_reference(golden):
+    from mplc.engine import CoalitionEngine
+    from itertools import combinations
+    total, exact_ref = 0, 0
+    for case in golden["cases"]:
+        sc = scenario_for(golden, case)
+        eng = CoalitionEngine.for_scenario(sc)
+        ds = sc.dataset
+        parts = [(p.x_train, p.y_train) for p in sc.partners_list]
+        n = case["partners_count"]
+        coals = [tuple(int(i) for i in k.split(",")) for k in case["values"]]
+        coals += [(p,) for p in range(n)]
+        if n <= 5:
+            coals += [c for r in range(2, n + 1) for c in combinations(range(n), r) if c not in coals]
+        res = eng.evaluate(coals, return_details=True)
+        for ci, c in enumerate(coals):
+            if len(c) == 1:
+                ref = olr.single_value(parts, c[0], ds.x_test, ds.y_test)
+                theta_ref = olr.fit_exact(*parts[c[0]])
+            else:
+                ref = olr.fedavg_value(parts, c, ds.x_test, ds.y_test)
+                sizes = [len(parts[p][1]) for p in c]
+                theta_ref = np.average(np.array([olr.fit_exact(*parts[p]) for p in c]), axis=0,
+                                       weights=np.asarray(sizes) / np.sum(sizes))
+            assert res["scores"][ci] == ref, (c, res["scores"][ci], ref)
+            assert np.max(np.abs(eng.last_theta[ci] - theta_ref)) < 1e-8
+            key = ",".join(map(str, c))
+            if key in case["values"]:
+                total += 1
+                exact_ref += res["scores"][ci] == case["values"][key]
+                assert abs(res["scores"][ci] - case["values"][key]) * len(ds.y_test) <= 1 + 1e-9
+        assert np.all(res["epochs_done"] == case["epoch_count"])
+    assert total == 71 and exact_ref >= 69
+
+
+@pytest.mark.gpu
+def test_titanic_exact_shapley_all_1023_coalitions():
+    """Config #2: 10 partners, exact Shapley over all 1023 coalitions in one launch; efficiency holds."""
+    from mplc.dataset import Titanic
+    from mplc.scenario import Scenario
+    from mplc.contributivity import Contributivity
+    sc = Scenario(10, [0.1] * 10, dataset=Titanic(synthetic=True), epoch_count=3, minibatch_count=1,
+                  is_early_stopping=False).provision()
+    c = Contributivity(scenario=sc)
+    c.compute_contributivity("Shapley values")
+    assert c.first_charac_fct_calls_count == 1023
+    assert abs(np.sum(c.contributivity_scores) - c.charac_fct_values[tuple(range(10))]) < 1e-12
