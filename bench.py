@@ -31,6 +31,20 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (v_mfma_f32_32x32x2_f32
 CONV_BWD_DATA_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2  # dA1 = dZ2 (*) W2 over all conv1 positions
 
 
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed PMC passes of this same bench command
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py); None when absent or for another workload."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = doc.get("kernels", {}).get(kernel)
+    if e is None or doc.get("workload") != workload:
+        return None
+    return int(e["traffic_bytes_per_launch"])
+
+
 def dist_init():
     import torch
     import torch.distributed as dist
@@ -297,8 +311,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline_shapley() if (world == 1 and not args.no_cpu_baseline) else None
     else:
         out, sc = bench_train(args, rank, world)
+        wl = out["config"]["workload"]
+        out["roofline"]["traffic"] = pmc_traffic(f"{args.profile_kernel}_kernel", wl)
         if not args.no_shapley_agg:
             agg = bench_shapley(args.n, 10, 2, rank, world)
+            agg["roofline"]["traffic"] = pmc_traffic("shapley_block_kernel", wl)
             out["shapley_agg"] = agg
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
