@@ -222,7 +222,7 @@ def bench_train(args, rank, world):
     from mplc.engine import CoalitionEngine
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
-    eng.evaluate([(0, 1)], epoch_count=1)  # untimed: module load, allocator warm-up
+    eng.warmup()  # untimed: code-object load (no training launch, so rocprof averages = timed launches)
     n = args.partners
     n_coal = 2 ** n - 1
 

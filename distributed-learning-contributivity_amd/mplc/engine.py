@@ -128,6 +128,16 @@ class CoalitionEngine:
             batches.append(cur)
         return batches
 
+    def warmup(self):
+        """Load the HIP code object (one tiny init_params launch) without running any training kernel."""
+        import torch
+        from . import _native
+        buf = torch.empty(STRIDE, dtype=torch.float32, device=self.device)
+        keys = torch.zeros(1, dtype=torch.int64, device=self.device)
+        _native.check(_native.lib().mplc_cnn_init_params(_native.ptr(buf), STRIDE, _native.ptr(keys), 1,
+                                                         _native.stream_handle(self.device)), "mplc_cnn_init_params")
+        torch.cuda.synchronize(self.device)
+
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):
         """v(S) (test accuracy, float64) for each coalition (sorted tuple of partner indices)."""
         coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
