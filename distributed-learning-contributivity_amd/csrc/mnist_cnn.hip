@@ -24,6 +24,7 @@
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float fvec4 __attribute__((ext_vector_type(4)));
 
 constexpr int IMG = 28;
 constexpr int A1 = 26;
@@ -49,6 +50,35 @@ __device__ __forceinline__ floatx16 zero16() {
   for (int i = 0; i < 16; ++i) z[i] = 0.0f;
   return z;
 }
+
+// conv1 weights as the MFMA B operand: lane (kh, ci) holds W1e[2s + kh][ci], s = 0..4, where W1e rows 0..8
+// are the 3x3 taps (ky*3 + kx) and row 9 is the bias.
+__device__ __forceinline__ void load_w1r(const float* __restrict__ P, int kh, int ci, float (&w1r)[5]) {
+#pragma unroll
+  for (int s = 0; s < 5; ++s) {
+    const int k = 2 * s + kh;
+    w1r[s] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : P[OFF_B1 + ci];
+  }
+}
+
+// conv1 + bias (pre-ReLU) of 32 positions on the fp32 MFMA: K = 9 taps + bias (patch value 1) in 5 k-steps.
+// Lane (kh, i) passes `pix`, the img_s offset of its position's top-left pixel (row stride IMG).
+// Result in accumulator layout: reg -> tile row (reg&3) + 8*(reg>>2) + 4*kh, column = channel lane&31.
+// All kernels that need conv1's output use this one routine, so forward and backward agree bit for bit.
+__device__ __forceinline__ floatx16 conv1_mfma(const float* img_s, int pix, int kh, const float (&w1r)[5]) {
+  floatx16 acc = zero16();
+  // tap k = 2s + kh at (k / 3) * IMG + k % 3
+  acc = mfma32(img_s[pix + (kh ? 1 : 0)], w1r[0], acc);
+  acc = mfma32(img_s[pix + (kh ? IMG : 2)], w1r[1], acc);
+  acc = mfma32(img_s[pix + (kh ? IMG + 2 : IMG + 1)], w1r[2], acc);
+  acc = mfma32(img_s[pix + (kh ? 2 * IMG + 1 : 2 * IMG)], w1r[3], acc);
+  const float a8 = img_s[pix + 2 * IMG + 2];
+  acc = mfma32(kh ? 1.0f : a8, w1r[4], acc);
+  return acc;
+}
+
+// accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
+__device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
 
 // ------------------------------------------------------------------------------------------------
 // Keyed index permutations (bit-identical restatement in oracle/cnn.py)
@@ -184,12 +214,11 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
 // ------------------------------------------------------------------------------------------------
 constexpr int FWD_THREADS = 192;
 
-__global__ __launch_bounds__(FWD_THREADS) void conv_fwd_kernel(
+__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, float* __restrict__ pooled,
     uint8_t* __restrict__ code) {
   __shared__ float img_s[16 * IMG];
-  __shared__ float w1_s[9 * C1 + C1];
   __shared__ float a1_s[14 * A1 * A1P];
   const int half = blockIdx.x;
   const int j = blockIdx.y;
@@ -201,26 +230,28 @@ __global__ __launch_bounds__(FWD_THREADS) void conv_fwd_kernel(
   const float* P = params + (int64_t)r * stride;
   const float* xi = x + (int64_t)row * (IMG * IMG) + half * 12 * IMG;
   for (int e = tid; e < 16 * IMG; e += FWD_THREADS) img_s[e] = xi[e];
-  for (int e = tid; e < 9 * C1 + C1; e += FWD_THREADS) w1_s[e] = P[OFF_W1 + e];
-  __syncthreads();
-  // conv1 + ReLU for local rows 0..13 (global 12*half + lr)
-  for (int e = tid; e < 14 * A1 * C1; e += FWD_THREADS) {
-    const int ci = e & 31;
-    const int pos = e >> 5;
-    const int lr = pos / A1, lc = pos % A1;
-    float acc = w1_s[9 * C1 + ci];
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) acc += img_s[(lr + ky) * IMG + lc + kx] * w1_s[(ky * 3 + kx) * C1 + ci];
-    a1_s[pos * A1P + ci] = fmaxf(acc, 0.0f);
-  }
-  __syncthreads();
-
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
+  float w1r[5];
+  load_w1r(P, kh, m, w1r);
+  __syncthreads();
+  // conv1 + ReLU for local rows 0..13 (global 12*half + lr): 364 positions = 12 MFMA tiles, 4 per wave
+  constexpr int NPOS1 = 14 * A1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = wave + 3 * u;
+    const int p = min(t * 32 + m, NPOS1 - 1);
+    const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int pw = t * 32 + acc_row(reg, kh);
+      if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
+    }
+  }
+  __syncthreads();
+
   int pbase[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -450,75 +481,94 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 // Dense(128) backward + Adam, per 64-row slice of W3 (block = 256 threads: row = tid/4, 32 cols each)
 // dp[j][k] = sum_c dh[j][c] W3[k][c];  dW3[k][c] = sum_j p[j][k] dh[j][c];  db3 (slice 0 block)
 // ------------------------------------------------------------------------------------------------
-constexpr int D1_ROWS = 64;
-constexpr int D1_SCHUNK = 32;
+constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
+constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
 __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
-  __shared__ float dh_s[D1_SCHUNK * HID];
+  __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
   __shared__ float p_s[D1_SCHUNK * D1_ROWS];
   const int r = blockIdx.y;
   const int k0 = blockIdx.x * D1_ROWS;
   const int count = cnt[r];
   if (count == 0) return;
   const int tid = threadIdx.x;
-  const int rowl = tid >> 2;
-  const int cq = (tid & 3) * 32;
-  float* W = params + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
-  float w[32], g[32];
+  const int rowl = tid >> 3;
+  // the 8 threads of a row own interleaved fvec4 chunks q = c8 + 8*i (columns 4q..4q+3): each global
+  // access instruction covers 128 contiguous bytes per row, each dh_s read 8 adjacent 16-B slots
+  const int c8 = tid & 7;
+  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
+  const bool fresh = cfg.reset;  // a fresh optimizer (first step of a round) never reads its moments
+  const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID;
+  fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c8;
+  fvec4* Mr = reinterpret_cast<fvec4*>(adam_m + roff) + c8;
+  fvec4* Vr = reinterpret_cast<fvec4*>(adam_v + roff) + c8;
+  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  // every HBM read of the pass is issued up front; the moments land while the gradient is accumulated
+  fvec4 w[4], g[4], mv[4], vv[4];
 #pragma unroll
-  for (int i = 0; i < 32; i += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(W + i);
-    w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
-    g[i] = g[i + 1] = g[i + 2] = g[i + 3] = 0.0f;
+  for (int i = 0; i < 4; ++i) {
+    w[i] = W[8 * i];
+    g[i] = z4;
+    mv[i] = z4;
+    vv[i] = z4;
+  }
+  if (!fresh) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mv[i] = __builtin_nontemporal_load(Mr + 8 * i);
+      vv[i] = __builtin_nontemporal_load(Vr + 8 * i);
+    }
   }
   const float* Pr = Pool + (int64_t)r * bmax * FEAT;
-  const float* dHr = dH + (int64_t)r * bmax * HID;
+  const fvec4* dHr = reinterpret_cast<const fvec4*>(dH + (int64_t)r * bmax * HID);
   float* dPr = dPool + (int64_t)r * bmax * FEAT;
   for (int c0 = 0; c0 < count; c0 += D1_SCHUNK) {
     const int cn = min(D1_SCHUNK, count - c0);
-    for (int e = tid; e < cn * HID; e += 256) dh_s[e] = dHr[(int64_t)c0 * HID + e];
+    for (int e = tid; e < cn * (HID / 4); e += 256) dh_s[e] = dHr[(int64_t)c0 * (HID / 4) + e];
     for (int e = tid; e < cn * D1_ROWS; e += 256) {
       const int jj = e / D1_ROWS, kk = e % D1_ROWS;
       p_s[e] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + kk];
     }
     __syncthreads();
+#pragma unroll 2
     for (int jj = 0; jj < cn; ++jj) {
       const float pv = p_s[jj * D1_ROWS + rowl];
       float d = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const float dh = dh_s[jj * HID + cq + i];
-        g[i] += pv * dh;
-        d += dh * w[i];
+      for (int i = 0; i < 4; ++i) {
+        const fvec4 dh = dh_s[jj * (HID / 4) + c8 + 8 * i];
+        g[i].x += pv * dh.x; g[i].y += pv * dh.y; g[i].z += pv * dh.z; g[i].w += pv * dh.w;
+        d += dh.x * w[i].x; d += dh.y * w[i].y; d += dh.z * w[i].z; d += dh.w * w[i].w;
       }
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
-      if ((tid & 3) == 0) dPr[(int64_t)(c0 + jj) * FEAT + k0 + rowl] = d;
+      d += __shfl_xor(d, 4, 64);
+      if (c8 == 0) dPr[(int64_t)(c0 + jj) * FEAT + k0 + rowl] = d;
     }
     __syncthreads();
   }
-  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
-  float* Mr = adam_m + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
-  float* Vr = adam_v + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID + cq;
 #pragma unroll
-  for (int i = 0; i < 32; i += 4) {
-    float4 mv = *reinterpret_cast<const float4*>(Mr + i);
-    float4 vv = *reinterpret_cast<const float4*>(Vr + i);
-    float pw[4] = {w[i], w[i + 1], w[i + 2], w[i + 3]};
-    float pm[4] = {mv.x, mv.y, mv.z, mv.w};
-    float pv[4] = {vv.x, vv.y, vv.z, vv.w};
+  for (int i = 0; i < 4; ++i) {
+    fvec4 pw = w[i];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) adam_apply(pw[q], pm[q], pv[q], g[i + q], cfg);
-    *reinterpret_cast<float4*>(W + i) = make_float4(pw[0], pw[1], pw[2], pw[3]);
-    *reinterpret_cast<float4*>(Mr + i) = make_float4(pm[0], pm[1], pm[2], pm[3]);
-    *reinterpret_cast<float4*>(Vr + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    for (int q = 0; q < 4; ++q) {
+      float p1 = pw[q], m1 = mv[i][q], v1 = vv[i][q];
+      adam_apply(p1, m1, v1, g[i][q], cfg);
+      pw[q] = p1;
+      mv[i][q] = m1;
+      vv[i][q] = v1;
+    }
+    W[8 * i] = pw;
+    __builtin_nontemporal_store(mv[i], Mr + 8 * i);
+    __builtin_nontemporal_store(vv[i], Vr + 8 * i);
   }
   if (blockIdx.x == 0 && tid < HID) {
     float gb = 0.0f;
-    for (int jj = 0; jj < count; ++jj) gb += dHr[(int64_t)jj * HID + tid];
+    const float* dHs = dH + (int64_t)r * bmax * HID;
+    for (int jj = 0; jj < count; ++jj) gb += dHs[(int64_t)jj * HID + tid];
     const int64_t o = (int64_t)r * stride + OFF_B3 + tid;
     adam_apply(params[o], adam_m[o], adam_v[o], gb, cfg);
   }
@@ -542,25 +592,48 @@ __global__ void transpose_w2_kernel(const float* __restrict__ params, int64_t st
 // ------------------------------------------------------------------------------------------------
 // conv2 data gradient + conv1 backward.  Block = (sample, band of 13 conv1 rows), 4 waves.
 // dA1[pos][ci] = sum_{ky,kx,co} dZ2[pos-(ky,kx)][co] W2[ky][kx][ci][co]  (implicit GEMM, K = 9 x 64)
-// dZ2 (the max-pool gradient, 3/4 zeros) is un-pooled ONCE per band and channel half into a dense LDS
-// tile [15 rows][24 cols][33], so the MFMA loop reads its A operand with one ds_read + one select (column
-// bound); B (W2 transposed, [kyx][co][ci]) streams from L2.  Epilogue: ReLU' of the recomputed conv1
-// output, then conv1's weight gradient partial sums per (sample, band).
+// dZ2 (the max-pool gradient, 3/4 zeros) is un-pooled from (dp, argmax code) into a dense LDS tile
+// [15 rows][28 cols (2 zero columns each side)][17] one quarter of the channels (16) at a time; every
+// A-operand read is then one ds_read_b32 at a compile-time offset from a per-lane base.  B (W2
+// transposed, [kyx][co][ci]) streams from L2.  The next quarter's (dp, code) are fetched into registers
+// while the current quarter's MFMAs run.  Epilogue on MFMA too: conv1 recomputed (conv1_mfma), ReLU'
+// applied, and dW1/db1 = patch^T dZ1 as 16 MFMAs per tile with the masked accumulators as B operand.
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_THREADS = 256;
 constexpr int BAND = 13;               // conv1 rows per block (2 bands cover 26 rows)
 constexpr int BAND_POS = BAND * A1;    // 338 positions
 constexpr int BAND_TILES = 11;         // ceil(338 / 32)
 constexpr int DZR = BAND + 2;          // dZ2 rows a band needs
-constexpr int DZP = 33;                // padded channel stride (32 channels per half)
+constexpr int DZC = Z2 + 4;            // dZ2 columns incl. 2 zero columns each side
+constexpr int DZQ = 17;                // padded channel stride (16 channels per quarter)
+constexpr int BWD_PRE = 6;             // pooled (dp, code) pairs per thread per quarter: 8 rows x 12 x 16 / 256
 
-__global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
+// One channel quarter of the dgrad GEMM for NT tiles (branch-free; NT is 3 for waves 0-2, 2 for wave 3).
+template <int NT>
+__device__ __forceinline__ void bwd_data_quarter(const float* dz_s, const int (&abase)[3], const float* Tq,
+                                                 floatx16 (&acc)[3]) {
+#pragma unroll
+  for (int kyx = 0; kyx < 9; ++kyx) {
+    const int ky = kyx / 3, kx = kyx % 3;
+    const int offA = ((2 - ky) * DZC + (2 - kx)) * DZQ;
+    const float* Tk = Tq + kyx * C2 * C1;
+    float b[8];
+#pragma unroll
+    for (int c2 = 0; c2 < 8; ++c2) b[c2] = Tk[2 * c2 * C1];
+#pragma unroll
+    for (int c2 = 0; c2 < 8; ++c2) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[u] = mfma32(dz_s[abase[u] + offA + 2 * c2], b[c2], acc[u]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_bwd_data_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     const float* __restrict__ params, int64_t stride, const float* __restrict__ w2t,
     const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
-  __shared__ float dz_s[DZR * Z2 * DZP];
+  __shared__ float dz_s[DZR * DZC * DZQ];
   __shared__ float img_s[(BAND + 2) * IMG];
-  __shared__ float w1_s[9 * C1 + C1];
   __shared__ float red_s[4][10 * 32];
   const int band = blockIdx.x & 1;
   const int j = blockIdx.x >> 1;
@@ -572,106 +645,90 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
   const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
   const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
   const int iy0 = band * BAND;
-  const int oy0 = iy0 - 2;  // dZ2 row of local row 0
+  const int oy0 = iy0 - 2;             // dZ2 row of local row 0
+  const int pr0 = (oy0 + 2) / 2 - 1;  // first pooled row touching the band (-1 or 5)
+  for (int e = tid; e < DZR * DZC * DZQ; e += BWD_THREADS) dz_s[e] = 0.0f;
   for (int e = tid; e < (BAND + 2) * IMG; e += BWD_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + iy0 * IMG + e];
-  for (int e = tid; e < 9 * C1 + C1; e += BWD_THREADS) w1_s[e] = P[OFF_W1 + e];
   const int lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31;
   const int kh = lane >> 5;
-  const float* T = w2t + (int64_t)r * (9 * C1 * C2);
-  // this wave's tiles: wave, wave+4, wave+8 (wave 3: two tiles)
+  // pooled pair e = tid + 256*s of a quarter: channel e&15, pooled col (e>>4)%12, pooled row pr0 + e/192
+  float pdv[BWD_PRE];
+  uint32_t pcd[BWD_PRE];
+  auto fetch = [&](int q) {
+#pragma unroll
+    for (int s = 0; s < BWD_PRE; ++s) {
+      const int e = tid + BWD_THREADS * s;
+      const int py = pr0 + e / 192;
+      const int pidx = (py * PL + (e >> 4) % PL) * C2 + q * 16 + (e & 15);
+      const bool ok = py >= 0 && py < PL;
+      pdv[s] = ok ? dp[pidx] : 0.0f;
+      pcd[s] = ok ? cd[pidx] : 0u;
+    }
+  };
+  fetch(0);
+  const float* T = w2t + (int64_t)r * (9 * C1 * C2) + kh * C1 + n;
   const int ntile = (wave + 8 < BAND_TILES) ? 3 : 2;
   floatx16 acc[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u) acc[u] = zero16();
-  int iyl[3], ixx[3];
-  bool valid[3];
+  int abase[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    const int pl = (wave + 4 * u) * 32 + n;
-    valid[u] = (u < ntile) && (pl < BAND_POS);
-    iyl[u] = pl / A1;  // local conv1 row (0..12)
-    ixx[u] = pl % A1;
+    acc[u] = zero16();
+    const int pl = min((wave + 4 * u) * 32 + n, BAND_POS - 1);
+    abase[u] = ((pl / A1) * DZC + pl % A1) * DZQ + kh;
   }
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();  // previous half's readers are done
-    for (int e = tid; e < DZR * Z2 * 32; e += BWD_THREADS) {
-      const int c = e & 31;
-      const int px = (e >> 5) % Z2;
-      const int lr = e / (32 * Z2);
-      const int oy = oy0 + lr;
-      float v = 0.0f;
-      if (oy >= 0 && oy < Z2) {
-        const int pidx = ((oy >> 1) * PL + (px >> 1)) * C2 + half * 32 + c;
-        const uint8_t cc = cd[pidx];
-        const int q = (oy & 1) * 2 + (px & 1);
-        if ((cc & 0x80) && (cc & 3) == q) v = dp[pidx];
-      }
-      dz_s[(lr * Z2 + px) * DZP + c] = v;
-    }
-    __syncthreads();
-    for (int kyx = 0; kyx < 9; ++kyx) {
-      const int ky = kyx / 3, kx = kyx % 3;
-      int base[3];
-      bool inb[3];
+  for (int q = 0; q < 4; ++q) {
+    __syncthreads();  // zero fill done / previous quarter's readers done
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int ox = ixx[u] - kx;
-        inb[u] = valid[u] && ox >= 0 && ox < Z2;
-        // dZ2 local row = (iy0 + iyl - ky) - oy0 = iyl - ky + 2  (0..14)
-        base[u] = inb[u] ? ((iyl[u] - ky + 2) * Z2 + ox) * DZP : 0;
-      }
-      const float* Tk = T + (kyx * C2 + half * 32) * C1 + n;
-#pragma unroll 8
-      for (int c2 = 0; c2 < 16; ++c2) {
-        const int c = 2 * c2 + kh;
-        const float b = Tk[c * C1];
+    for (int s = 0; s < BWD_PRE; ++s) {
+      const int e = tid + BWD_THREADS * s;
+      const int py = pr0 + e / 192;
+      const int pc = (e >> 4) % PL;
+      const int ch = e & 15;
+      const uint32_t c = pcd[s];
+      const float v = (c & 0x80) ? pdv[s] : 0.0f;
+      const int sel = c & 3;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const float a = inb[u] ? dz_s[base[u] + c] : 0.0f;
-          acc[u] = mfma32(a, b, acc[u]);
+      for (int dy = 0; dy < 2; ++dy) {
+        const int lr = 2 * py + dy - oy0;
+        if (py >= 0 && py < PL && lr >= 0 && lr < DZR) {
+          float* d = dz_s + (lr * DZC + 2 * pc + 2) * DZQ + ch;
+          d[0] = (sel == 2 * dy) ? v : 0.0f;
+          d[DZQ] = (sel == 2 * dy + 1) ? v : 0.0f;
         }
       }
     }
+    if (q < 3) fetch(q + 1);
+    __syncthreads();
+    if (ntile == 3) bwd_data_quarter<3>(dz_s, abase, T + q * 16 * C1, acc);
+    else bwd_data_quarter<2>(dz_s, abase, T + q * 16 * C1, acc);
   }
-  // epilogue: ReLU' of the recomputed conv1 output, conv1 weight gradient
-  float gw1[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) gw1[i] = 0.0f;
-  float gb1 = 0.0f;
-  const int ci = n;
+  // epilogue: dZ1 = dA1 * ReLU'(conv1), then [dW1 | db1] += patch^T dZ1 on MFMA (rows = 9 taps + bias)
+  float w1r[5];
+  load_w1r(P, kh, n, w1r);
+  const int toff = (n < 9) ? (n / 3) * IMG + n % 3 : 0;
+  floatx16 g = zero16();
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
     if (u >= ntile) break;
     const int t = wave + 4 * u;
+    const int pl = min(t * 32 + n, BAND_POS - 1);
+    const floatx16 a1 = conv1_mfma(img_s, (pl / A1) * IMG + pl % A1, kh, w1r);
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int pl = t * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * kh;
-      if (pl < BAND_POS) {
-        const int py = pl / A1, px = pl % A1;  // local row py (image rows py..py+2 in img_s)
-        float a1 = w1_s[9 * C1 + ci];
-        float pix[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-          pix[k] = img_s[(py + k / 3) * IMG + px + k % 3];
-          a1 += pix[k] * w1_s[k * C1 + ci];
-        }
-        if (a1 > 0.0f) {
-          const float dz = acc[u][reg];
-#pragma unroll
-          for (int k = 0; k < 9; ++k) gw1[k] += pix[k] * dz;
-          gb1 += dz;
-        }
-      }
+      const int pr = t * 32 + acc_row(reg, kh);
+      const float dz = (a1[reg] > 0.0f) ? acc[u][reg] : 0.0f;
+      const int prc = min(pr, BAND_POS - 1);
+      const float pv = img_s[(prc / A1) * IMG + prc % A1 + toff];
+      const float av = (pr < BAND_POS && n < 10) ? (n < 9 ? pv : 1.0f) : 0.0f;
+      g = mfma32(av, dz, g);
     }
   }
+  // g: rows = tap (0..9), cols = ci; rows 0..9 live in regs 0..3 (kh 0: rows 0-3, kh 1: rows 4-7), 4..5 (kh 0)
 #pragma unroll
-  for (int k = 0; k < 9; ++k) gw1[k] += __shfl_xor(gw1[k], 32, 64);
-  gb1 += __shfl_xor(gb1, 32, 64);
-  if (kh == 0) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) red_s[wave][k * 32 + n] = gw1[k];
-    red_s[wave][9 * 32 + n] = gb1;
+  for (int reg = 0; reg < 8; ++reg) {
+    const int k = acc_row(reg, kh);
+    if (k < 10) red_s[wave][k * 32 + n] = g[reg];
   }
   __syncthreads();
   float* out = w1_part + (((int64_t)r * bmax + j) * 2 + band) * MPLC_CNN_W1P;
@@ -681,21 +738,24 @@ __global__ __launch_bounds__(BWD_THREADS) void conv_bwd_data_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // conv2 weight gradient: dW2[kyx*32+ci][co] = sum_px a1[py+ky][px+kx][ci] dZ2[px][co]; db2.
-// Block = (split s, replica r): samples [8s, 8s+8); 3 waves x (3 row tiles x 2 col tiles).
-// Output rows of 4 conv2 pixels-rows at a time (a band): conv1 rows recomputed into LDS per band.
+// Block = (split s, replica r): samples [8s, 8s+8); 3 waves, wave w owns rows ky = w (kx = 0..2) x 64 co.
+// Per band of 4 conv2 rows: conv1 rows recomputed on MFMA (conv1_mfma) into LDS, dZ2 un-pooled from the
+// prefetched (dp, code) registers; the K loop over the band's 96 pixels is fully unrolled (compile-time
+// LDS offsets).  The next band's (dp, code) are fetched while the current band's MFMAs run.
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_THREADS = 192;
 constexpr int WG_SAMPLES = 8;  // samples per wgrad split (fixed: reproducible sums)
 constexpr int WGP = 65;        // padded channel stride of the dense dZ2 band
+constexpr int WG_PRE = 8;      // pooled pairs per thread per band: 2 rows x 12 x 64 / 192
 
-__global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
   __shared__ float img_s[IMG * IMG];
-  __shared__ float w1_s[9 * C1 + C1];
   __shared__ float a1_s[6 * A1 * C1];
   __shared__ float dzd_s[4 * Z2 * WGP];  // dense un-pooled dZ2 of the band: [4 rows][24 cols][65]
+  __shared__ float gb_s[3][C2];
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -703,64 +763,87 @@ __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
   // so its summation order (and v(S)) does not depend on which other replicas share the launch
   const int j_begin = sp * WG_SAMPLES;
   const int j_end = min(count, j_begin + WG_SAMPLES);
+  if (j_begin >= j_end) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
   const float* P = params + (int64_t)r * stride;
-  for (int e = tid; e < 9 * C1 + C1; e += WG_THREADS) w1_s[e] = P[OFF_W1 + e];
+  float w1r[5];
+  load_w1r(P, kh, m, w1r);
   floatx16 acc[3][2];
 #pragma unroll
   for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
-  float gb[2] = {0.0f, 0.0f};
+  float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread un-pools has that channel)
+  float pdv[WG_PRE];
+  uint32_t pcd[WG_PRE];
+  // pooled rows 2*band, 2*band+1 of sample jj: pair e = tid + 192*s is element 24*64*band + e (contiguous)
+  auto fetch = [&](int jj, int band) {
+    const int64_t base = ((int64_t)r * bmax + jj) * FEAT + band * 2 * PL * C2;
+#pragma unroll
+    for (int s = 0; s < WG_PRE; ++s) {
+      const int e = tid + WG_THREADS * s;
+      pdv[s] = dPool[base + e];
+      pcd[s] = code[base + e];
+    }
+  };
+  fetch(j_begin, 0);
+  // A-operand bases: row tile u = (ky = wave, kx = u) x 32 ci, lane (kh, m) reads pixel px0 + kh, channel m
+  const int zb = kh * WGP + m;
+  int ab[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) ab[u] = (wave * A1 + u) * C1 + kh * C1 + m;
   for (int j = j_begin; j < j_end; ++j) {
     const int row = idx[(int64_t)r * bmax + j];
-    const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
-    const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
-    __syncthreads();
     for (int e = tid; e < IMG * IMG; e += WG_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + e];
     for (int band = 0; band < 6; ++band) {
-      __syncthreads();
-      // conv1 rows 4*band .. 4*band+5 and pooled rows 2*band, 2*band+1
-      for (int e = tid; e < 6 * A1 * C1; e += WG_THREADS) {
-        const int ci = e & 31;
-        const int pos = e >> 5;
-        const int lr = pos / A1, lc = pos % A1;
-        const int gy = 4 * band + lr;
-        float a = w1_s[9 * C1 + ci];
+      __syncthreads();  // img_s loaded; previous band's MFMA readers done
 #pragma unroll
-        for (int k = 0; k < 9; ++k) a += img_s[(gy + k / 3) * IMG + lc + k % 3] * w1_s[k * C1 + ci];
-        a1_s[e] = fmaxf(a, 0.0f);
-      }
-      for (int e = tid; e < 4 * Z2 * C2; e += WG_THREADS) {
+      for (int s = 0; s < WG_PRE; ++s) {
+        const int e = tid + WG_THREADS * s;
         const int co = e & 63;
-        const int px = (e >> 6) % Z2;
-        const int oyl = e / (64 * Z2);
-        const int oy = 4 * band + oyl;
-        const int pidx = ((oy >> 1) * PL + (px >> 1)) * C2 + co;
-        const uint8_t c = cd[pidx];
-        const int q = (oy & 1) * 2 + (px & 1);
-        dzd_s[(oyl * Z2 + px) * WGP + co] = ((c & 0x80) && (c & 3) == q) ? dp[pidx] : 0.0f;
+        const int pc = (e >> 6) % PL;
+        const int prr = e / (PL * C2);
+        const uint32_t c = pcd[s];
+        const float v = (c & 0x80) ? pdv[s] : 0.0f;
+        gb += v;
+        const int sel = c & 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dzd_s[((2 * prr + (q >> 1)) * Z2 + 2 * pc + (q & 1)) * WGP + co] = (sel == q) ? v : 0.0f;
       }
+      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles (waves 0,1: two; wave 2: one)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 3 * u;
+        if (t < 5) {
+          const int p = min(t * 32 + m, 6 * A1 - 1);
+          const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int pw = t * 32 + acc_row(reg, kh);
+            if (pw < 6 * A1) a1_s[pw * C1 + m] = fmaxf(a[reg], 0.0f);
+          }
+        }
+      }
+      if (band < 5) fetch(j, band + 1);
+      else if (j + 1 < j_end) fetch(j + 1, 0);
       __syncthreads();
-      // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh)
-#pragma unroll 4
-      for (int s = 0; s < 48; ++s) {
-        const int px = 2 * s + kh;          // 0..95 within band
-        const int oyl = px / Z2, ox = px % Z2;  // oyl 0..3
-        const float bz0 = dzd_s[(oyl * Z2 + ox) * WGP + m];
-        const float bz1 = dzd_s[(oyl * Z2 + ox) * WGP + 32 + m];
-        if (wave == 0) { gb[0] += bz0; gb[1] += bz1; }
+      // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh): px = 2*s2 + kh
+#pragma unroll
+      for (int s2 = 0; s2 < 48; ++s2) {
+        const int oyl = (2 * s2) / Z2, ox0 = (2 * s2) % Z2;
+        const float bz0 = dzd_s[zb + (oyl * Z2 + ox0) * WGP];
+        const float bz1 = dzd_s[zb + (oyl * Z2 + ox0) * WGP + 32];
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
-          const int kyx = 3 * wave + u;     // row tile = 32 consecutive (kyx, ci)
-          const int ky = kyx / 3, kx = kyx % 3;
-          const float a = a1_s[((oyl + ky) * A1 + ox + kx) * C1 + m];
+          const float a = a1_s[ab[u] + (oyl * A1 + ox0) * C1];
           acc[u][0] = mfma32(a, bz0, acc[u][0]);
           acc[u][1] = mfma32(a, bz1, acc[u][1]);
         }
       }
     }
+    __syncthreads();  // last band's readers done before the next sample's img_s load
   }
   float* out = w2_part + ((int64_t)r * splits + sp) * MPLC_CNN_W2P;
 #pragma unroll
@@ -770,19 +853,14 @@ __global__ __launch_bounds__(WG_THREADS) void conv_wgrad_kernel(
     for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int ci = (reg & 3) + 8 * (reg >> 2) + 4 * kh;
+        const int ci = acc_row(reg, kh);
         out[(kyx * C1 + ci) * C2 + nt * 32 + m] = acc[u][nt][reg];
       }
     }
   }
-  if (wave == 0) {
-    gb[0] += __shfl_xor(gb[0], 32, 64);
-    gb[1] += __shfl_xor(gb[1], 32, 64);
-    if (kh == 0) {
-      out[9 * C1 * C2 + m] = gb[0];
-      out[9 * C1 * C2 + 32 + m] = gb[1];
-    }
-  }
+  gb_s[wave][lane] = gb;
+  __syncthreads();
+  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + gb_s[2][tid];
 }
 
 // Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
