@@ -1,0 +1,1056 @@
+// Batched multi-model CIFAR10 CNN trainer for gfx950 (contract: include/mplc_hip_cifar.h).
+//
+// One lockstep step of R replicas (each with its own weights, batch, schedule and dropout masks):
+//   schedule       per replica: sample rows, batch count, optimizer iteration, dropout key
+//   conv1_fwd      x -> a1 = relu(conv3x3 same, 3->32)                      implicit GEMM, fp32 MFMA
+//   conv2_fwd      a1 -> d2 = dropout(pool(relu(conv3x3 valid, 32->32)))   pool fused in the accumulator
+//   conv3_fwd      d2 -> a3 = relu(conv3x3 same, 32->64)
+//   conv4_fwd      a3 -> d4 = dropout(pool(relu(conv3x3 valid, 64->64)))
+//   dense5_fwd     d4 -> d5 = dropout(relu(d4 W5 + b5))                   A in LDS, W5 streamed
+//   head           Dense(10) + softmax-CE gradient, dW6 + RMSprop, dh5 = (dl W6^T) * dropout' * relu'
+//   dense5_bwd     per 16-row slice of W5: dd4 = dh5 W5^T, dW5 = d4^T dh5, RMSprop(W5) in one pass; the
+//                  epilogue routes dd4 through dropout' and the pool into the dense dz4 (relu' included)
+//   transpose_w    W2|W3|W4 -> flipped [kyx'][co][ci] for the data-gradient GEMMs
+//   conv4 wgrad/dgrad, conv3 wgrad/dgrad (epilogue: dropout' + un-pool into dz2), conv2 wgrad/dgrad,
+//   conv1 wgrad    data gradients are the same implicit-GEMM kernel as the forward (full/same padding,
+//                  flipped weights) with a relu'-mask epilogue; weight gradients are split-K over fixed
+//                  groups of MPLC_CIFAR_WG_SAMPLES samples (sums independent of the batch composition)
+//   rmsprop_small  RMSprop on W1..b4 from the split partials (fixed order: bitwise reproducible)
+// Everything is fp32 (the reference's Keras float32), accumulated on the exact-f32 MFMA 32x32x2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "keyed.h"
+#include "mplc_hip.h"
+#include "mplc_hip_cifar.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float fvec4 __attribute__((ext_vector_type(4)));
+
+constexpr int64_t OFF_W1 = MPLC_CIFAR_OFF_W1, OFF_B1 = MPLC_CIFAR_OFF_B1, OFF_W2 = MPLC_CIFAR_OFF_W2,
+                  OFF_B2 = MPLC_CIFAR_OFF_B2, OFF_W3 = MPLC_CIFAR_OFF_W3, OFF_B3 = MPLC_CIFAR_OFF_B3,
+                  OFF_W4 = MPLC_CIFAR_OFF_W4, OFF_B4 = MPLC_CIFAR_OFF_B4, OFF_W5 = MPLC_CIFAR_OFF_W5,
+                  OFF_B5 = MPLC_CIFAR_OFF_B5, OFF_W6 = MPLC_CIFAR_OFF_W6, OFF_B6 = MPLC_CIFAR_OFF_B6;
+constexpr int64_t STRIDE = MPLC_CIFAR_STRIDE;
+constexpr int IMG_SZ = 32 * 32 * 3;
+constexpr int FEAT = MPLC_CIFAR_D4;  // 2304
+constexpr int HID = MPLC_CIFAR_H5;   // 512
+constexpr int NCLS = 10;
+constexpr int WGS = MPLC_CIFAR_WG_SAMPLES;
+constexpr int WPART = MPLC_CIFAR_WPART;
+// flipped weights for the data gradients, per replica: W2f @0 [9][32][32], W3f @9216 [9][64][32], W4f @27648
+constexpr int WT_W2 = 0, WT_W3 = 9216, WT_W4 = 27648;
+
+// dropout (Keras Dropout -> tf.nn.dropout: (x * (1/(1-rate))) * (u >= rate)); u = 24-bit keyed counter
+constexpr uint32_t DROP_L2 = 2, DROP_L4 = 4, DROP_L5 = 5;
+constexpr uint32_t THR_25 = 1u << 22;  // 0.25 * 2^24
+constexpr uint32_t THR_50 = 1u << 23;  // 0.5 * 2^24
+constexpr float SCALE_25 = 0x1.555556p+0f;  // float(1 / 0.75)
+constexpr float SCALE_50 = 2.0f;
+constexpr uint8_t CODE_KEEP = 0x40, CODE_POS = 0x80;
+
+__device__ __forceinline__ bool drop_keep(uint64_t dkey, uint32_t layer, uint32_t j, uint32_t e, uint32_t thr) {
+  const uint64_t h = mix64(dkey ^ mix64(((uint64_t)layer << 56) | ((uint64_t)j << 32) | (uint64_t)e));
+  return (uint32_t)(h >> 40) >= thr;
+}
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.0f;
+  return z;
+}
+
+// accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
+__device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
+
+// ------------------------------------------------------------------------------------------------
+// Keras 2.3.1 RMSprop (keras/optimizers.py): lr_t = lr / (1 + decay * iterations) with the iteration
+// count before this update; a = rho a + (1 - rho) g^2; p -= lr_t g / (sqrt(a) + eps).  (1 - rho) comes
+// from the host (a Python double rounded once to fp32, as Keras does).  A fresh optimizer (FedAvg partner
+// fit, t == 1) has a == 0.
+// ------------------------------------------------------------------------------------------------
+struct RmsCfg {
+  float lr_t, rho, one_m_rho, eps;
+  bool reset;
+};
+
+__device__ __forceinline__ RmsCfg rms_cfg(int t, float lr, float rho, float omr, float decay, float eps) {
+  RmsCfg c;
+  const float it = (float)(t - 1);
+  c.lr_t = lr * (1.0f / (1.0f + decay * it));
+  c.rho = rho;
+  c.one_m_rho = omr;
+  c.eps = eps;
+  c.reset = (t == 1);
+  return c;
+}
+
+__device__ __forceinline__ void rms_apply(float& p, float& a, float g, const RmsCfg& c) {
+  const float a0 = c.reset ? 0.0f : a;
+  const float an = c.rho * a0 + c.one_m_rho * (g * g);
+  p = p - c.lr_t * g / (sqrtf(an) + c.eps);
+  a = an;
+}
+
+// ------------------------------------------------------------------------------------------------
+// init (glorot_uniform from mix64(key + i*golden), as mplc_cnn_init_params), schedule, flipped weights
+// ------------------------------------------------------------------------------------------------
+__global__ void init_params_kernel(float* __restrict__ params, int64_t stride, const uint64_t* __restrict__ keys) {
+  const int m = blockIdx.y;
+  const uint64_t key = keys[m];
+  float* row = params + (int64_t)m * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += (int64_t)gridDim.x * blockDim.x) {
+    float lim = 0.0f;
+    if (i < OFF_W1 + 864) lim = 0x1.1aa69ep-3f;
+    else if (i >= OFF_W2 && i < OFF_W2 + 9216) lim = 0x1.a20bd8p-4f;
+    else if (i >= OFF_W3 && i < OFF_W3 + 18432) lim = 0x1.555556p-4f;
+    else if (i >= OFF_W4 && i < OFF_W4 + 36864) lim = 0x1.279a74p-4f;
+    else if (i >= OFF_W5 && i < OFF_W5 + 1179648) lim = 0x1.7a2316p-5f;
+    else if (i >= OFF_W6 && i < OFF_W6 + 5120) lim = 0x1.b72326p-4f;
+    float w = 0.0f;
+    if (lim != 0.0f) {
+      const uint64_t hsh = mix64(key + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+      const float u = (float)(uint32_t)(hsh >> 40) * 0x1p-24f;
+      w = (u * 2.0f - 1.0f) * lim;
+    }
+    row[i] = w;
+  }
+}
+
+__global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_rep, int bmax,
+                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits, int step,
+                                int M, int round_len, int epochs, int32_t* __restrict__ idx,
+                                int32_t* __restrict__ cnt, int32_t* __restrict__ opt_t,
+                                uint64_t* __restrict__ drop_key) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)n_rep * bmax) return;
+  const int r = (int)(gid / bmax);
+  const int j = (int)(gid % bmax);
+  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits);
+  idx[gid] = ss.row;
+  if (j == 0) {
+    cnt[r] = ss.c;
+    opt_t[r] = ss.at;
+    drop_key[r] = ss.dkey;
+  }
+}
+
+// wt[kyx'][co][ci] = W[8 - kyx'][ci][co] for W2 (32x32), W3 (32x64), W4 (64x64)
+__global__ void transpose_w_kernel(const float* __restrict__ params, const int32_t* __restrict__ cnt,
+                                   float* __restrict__ wt) {
+  const int r = blockIdx.y;
+  if (cnt[r] == 0) return;
+  const float* P = params + (int64_t)r * STRIDE;
+  float* T = wt + (int64_t)r * MPLC_CIFAR_WT;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < MPLC_CIFAR_WT; e += gridDim.x * blockDim.x) {
+    int ci_n, co_n, base, off;
+    if (e < WT_W3) { ci_n = 32; co_n = 32; base = WT_W2; off = OFF_W2; }
+    else if (e < WT_W4) { ci_n = 32; co_n = 64; base = WT_W3; off = OFF_W3; }
+    else { ci_n = 64; co_n = 64; base = WT_W4; off = OFF_W4; }
+    const int l = e - base;
+    const int kyx = l / (ci_n * co_n);
+    const int rem = l % (ci_n * co_n);
+    const int co = rem / ci_n, ci = rem % ci_n;
+    T[e] = P[off + ((8 - kyx) * ci_n + ci) * co_n + co];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// 3x3 stride-1 convolution as an implicit GEMM on v_mfma_f32_32x32x2f32:
+//   out[y][x][n] = sum_{ky,kx,c} in[y+ky-PAD][x+kx-PAD][c] * B[(ky*3+kx)*CI + c][n]
+// Forward: B = W [ky][kx][ci][co].  Data gradient: in = dZ of the layer, PAD' = 2 - PAD, B = flipped W.
+// Block = (row band, sample slot j, replica r), NW waves; the band's input rows are staged in LDS
+// ([rows][cols][CI|1], odd channel stride: the 32 lanes of a half read 32 pixels on 32 banks); B streams
+// from L2.  GEMM rows: output pixels of the band, or for the pooled forward 2x2 windows x 4 pixels laid
+// out so that the 4 pixels of a window are accumulator registers 4g..4g+3 of one lane (pool = register
+// max).  Wave w owns the row tiles w + NW*u, u < UM, and all CO/32 column tiles.
+// ------------------------------------------------------------------------------------------------
+enum { EPI_FWD = 0, EPI_FWD_POOL = 1, EPI_BWD_MASK = 2, EPI_BWD_UNPOOL = 3 };
+
+struct ConvArgs {
+  const float* in;
+  int in_mode;  // 0: slot-major activations [r*bmax + j]; 1: dataset row idx[r*bmax + j]; 2: row_base + j
+  int row_base;
+  const int32_t* idx;
+  const int32_t* cnt;  // per replica sample count (NULL: cnt_all)
+  int cnt_all;
+  int bmax;
+  const float* w;      // B operand of replica r: w + r * w_rstride
+  int64_t w_rstride;
+  const float* bias;   // forward: bias of replica r: bias + r * b_rstride
+  int64_t b_rstride;
+  const uint64_t* drop_key;  // pooled forward, train: per replica dropout key (NULL: inference)
+  uint32_t drop_layer;
+  const float* aux;          // BWD_MASK: the layer input activation (relu output) [slot][HO*WO*CO]
+  const uint8_t* code_in;    // BWD_UNPOOL: pool/dropout code of the grid [slot][HO*WO*CO]
+  float* out;
+  uint8_t* code_out;         // pooled forward, train
+};
+
+__host__ __device__ constexpr int ci3_off(int k, int wip) { return ((k / 9) * wip + (k / 3) % 3) * 3 + k % 3; }
+
+template <int HI, int WI, int CI, int CO, int PAD, int BR, int NW, int UM, int EPI>
+__global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
+  constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
+  constexpr bool POOL = (EPI == EPI_FWD_POOL);
+  constexpr int PH = HO / 2, PW = WO / 2;
+  constexpr int ROWS = POOL ? 2 * BR : BR;  // output rows per band
+  constexpr int LR = ROWS + 2, WIP = WI + 2 * PAD, CIP = CI | 1;
+  constexpr int NT = CO / 32;
+  constexpr int MROWS = POOL ? BR * PW * 4 : BR * WO;
+  constexpr int NTHR = NW * 64;
+  static_assert(NW * UM * 32 >= MROWS, "row tiles do not cover the band");
+  static_assert(CO % 32 == 0 && (CI == 3 || CI % 2 == 0), "unsupported channel counts");
+  __shared__ float in_s[LR * WIP * CIP];
+  const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+  const int count = a.cnt ? a.cnt[r] : a.cnt_all;
+  if (j >= count) return;
+  const int tid = threadIdx.x;
+  const int64_t slot = (int64_t)r * a.bmax + j;
+  constexpr int IN_SZ = HI * WI * CI;
+  const float* src = a.in_mode == 1 ? a.in + (int64_t)a.idx[slot] * IN_SZ
+                     : a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ
+                                      : a.in + slot * IN_SZ;
+  const int y0 = band * ROWS;
+  for (int e = tid; e < LR * WIP * CI; e += NTHR) {
+    const int c = e % CI;
+    const int col = (e / CI) % WIP;
+    const int rr = e / (CI * WIP);
+    const int iy = y0 - PAD + rr, ix = col - PAD;
+    float v = 0.0f;
+    if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
+    in_s[(rr * WIP + col) * CIP + c] = v;
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31, kh = lane >> 5;
+  int abase[UM];
+#pragma unroll
+  for (int u = 0; u < UM; ++u) {
+    const int p = (wave + NW * u) * 32 + n;
+    int yl, x;
+    bool ok;
+    if (POOL) {
+      const int w = p >> 2, q = p & 3;
+      const int pyl = w / PW;
+      yl = 2 * pyl + (q >> 1);
+      x = 2 * (w % PW) + (q & 1);
+      ok = p < MROWS && band * BR + pyl < PH;
+    } else {
+      yl = p / WO;
+      x = p % WO;
+      ok = p < MROWS && y0 + yl < HO;
+    }
+    if (!ok) { yl = 0; x = 0; }
+    abase[u] = (yl * WIP + x) * CIP + (CI == 3 ? 0 : kh);
+  }
+  floatx16 acc[UM][NT];
+#pragma unroll
+  for (int u = 0; u < UM; ++u)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[u][nt] = zero16();
+  const float* W = a.w + (int64_t)r * a.w_rstride;
+  __syncthreads();
+  if constexpr (CI == 3) {
+    // K = 27 taps x channels, padded to 28: lane half kh takes k = 2s + kh
+    const float* Wl = W + kh * CO + n;
+#pragma unroll
+    for (int s = 0; s < 14; ++s) {
+      const bool valid = (2 * s + kh) < 27;
+      const int off = kh ? (2 * s + 1 < 27 ? ci3_off(2 * s + 1, WIP) : 0) : ci3_off(2 * s, WIP);
+      const float b = valid ? Wl[2 * s * CO] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < UM; ++u) {
+        const float av = valid ? in_s[abase[u] + off] : 0.0f;
+        acc[u][0] = mfma32(av, b, acc[u][0]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int kyx = 0; kyx < 9; ++kyx) {
+      const int offA = ((kyx / 3) * WIP + kyx % 3) * CIP;
+      const float* Wk = W + (int64_t)(kyx * CI + kh) * CO + n;
+#pragma unroll
+      for (int c2 = 0; c2 < CI / 2; ++c2) {
+        float b[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b[nt] = Wk[2 * c2 * CO + nt * 32];
+#pragma unroll
+        for (int u = 0; u < UM; ++u) {
+          const float av = in_s[abase[u] + offA + 2 * c2];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[u][nt] = mfma32(av, b[nt], acc[u][nt]);
+        }
+      }
+    }
+  }
+  // ---- epilogues ----
+  if constexpr (EPI == EPI_FWD) {
+    const float* bias = a.bias + (int64_t)r * a.b_rstride;
+    float* o = a.out + slot * (HO * WO * CO);
+#pragma unroll
+    for (int u = 0; u < UM; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const float bv = bias[nt * 32 + n];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
+          const int y = y0 + p / WO, x = p % WO;
+          if (p < MROWS && y < HO) o[(y * WO + x) * CO + nt * 32 + n] = fmaxf(acc[u][nt][reg] + bv, 0.0f);
+        }
+      }
+  } else if constexpr (EPI == EPI_FWD_POOL) {
+    const float* bias = a.bias + (int64_t)r * a.b_rstride;
+    float* o = a.out + slot * (PH * PW * CO);
+    uint8_t* oc = a.drop_key ? a.code_out + slot * (PH * PW * CO) : nullptr;
+    const uint64_t dkey = a.drop_key ? a.drop_key[r] : 0ull;
+#pragma unroll
+    for (int u = 0; u < UM; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = nt * 32 + n;
+        const float bv = bias[co];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int wl = (wave + NW * u) * 8 + 2 * g + kh;
+          const int pyl = wl / PW, px = wl % PW;
+          const int py = band * BR + pyl;
+          if (wl * 4 < MROWS && py < PH) {
+            float best = acc[u][nt][4 * g] + bv;
+            int arg = 0;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const float z = acc[u][nt][4 * g + q] + bv;
+              if (z > best) { best = z; arg = q; }
+            }
+            const int pidx = (py * PW + px) * CO + co;
+            const float av = fmaxf(best, 0.0f);
+            if (oc) {
+              const bool keep = drop_keep(dkey, a.drop_layer, (uint32_t)j, (uint32_t)pidx, THR_25);
+              o[pidx] = keep ? av * SCALE_25 : 0.0f;
+              oc[pidx] = (uint8_t)(arg | (keep ? CODE_KEEP : 0) | (best > 0.0f ? CODE_POS : 0));
+            } else {
+              o[pidx] = av;
+            }
+          }
+        }
+      }
+  } else if constexpr (EPI == EPI_BWD_MASK) {
+    const float* act = a.aux + slot * (HO * WO * CO);
+    float* o = a.out + slot * (HO * WO * CO);
+#pragma unroll
+    for (int u = 0; u < UM; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
+          const int y = y0 + p / WO, x = p % WO;
+          if (p < MROWS && y < HO) {
+            const int o_i = (y * WO + x) * CO + nt * 32 + n;
+            o[o_i] = act[o_i] > 0.0f ? acc[u][nt][reg] : 0.0f;
+          }
+        }
+  } else {  // EPI_BWD_UNPOOL: grid = pooled+dropout grid of the layer below; out = its dense dZ (2HO x 2WO)
+    const uint8_t* cd = a.code_in + slot * (HO * WO * CO);
+    float* o = a.out + slot * (4 * HO * WO * CO);
+#pragma unroll
+    for (int u = 0; u < UM; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
+          const int y = y0 + p / WO, x = p % WO;
+          if (p < MROWS && y < HO) {
+            const int ch = nt * 32 + n;
+            const uint32_t c = cd[(y * WO + x) * CO + ch];
+            const float v = (c & CODE_KEEP) ? acc[u][nt][reg] * SCALE_25 : 0.0f;
+            const bool pos = (c & CODE_POS) != 0;
+            const int sel = c & 3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              o[((2 * y + (q >> 1)) * (2 * WO) + 2 * x + (q & 1)) * CO + ch] = (pos && sel == q) ? v : 0.0f;
+          }
+        }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient of a 3x3 conv: dW[kyx][ci][co] = sum_{samples, pixels} X[p + (ky,kx) - PAD][ci] dZ[p][co],
+// db[co] = sum dZ.  Block = (split sp, replica r): samples [WGS*sp, WGS*sp + WGS) in order, row bands of BR
+// output rows; X band and dZ band staged in LDS (dZ rows padded to an even width WOE with zeros so a
+// k-pair never straddles rows); the band's K loop is fully unrolled (compile-time LDS offsets).  Only the
+// first HOV x WOV output pixels are used (conv4: row/col 12 are dropped by the pool, their dZ is 0).
+// Row tiles: (kyx, 32 input channels); wave w owns row tiles w + NW*u and all CO/32 column tiles.  For
+// CI = 3 (conv1) the 27 rows fit one tile and the waves split the band's rows instead (KSPLIT), reduced in
+// LDS in wave order.  db: each thread sums the dZ elements it stages (fixed channel), reduced in order.
+// ------------------------------------------------------------------------------------------------
+struct WgArgs {
+  const float* x;
+  int x_mode;  // 0 slot-major activations, 1 dataset rows via idx
+  const int32_t* idx;
+  const int32_t* cnt;
+  int bmax;
+  int splits;
+  const float* dz;
+  float* wpart;
+  int off_w, off_b;
+};
+
+template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BR, int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
+  constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
+  constexpr int WOE = WOV + (WOV & 1);
+  constexpr int WXP = WI + 2 * PAD + 1;
+  constexpr int NT = CO / 32;
+  constexpr bool KSPLIT = (CI == 3);
+  constexpr int MT = KSPLIT ? 1 : 9 * CI / 32;
+  constexpr int UMW = KSPLIT ? 1 : MT / NW;
+  constexpr int NTHR = NW * 64;
+  constexpr int NB = (HOV + BR - 1) / BR;
+  constexpr int RW = KSPLIT ? BR / NW : BR;  // rows of the band per wave
+  constexpr int SW = RW * WOE / 2;           // k-steps per wave per band
+  static_assert(KSPLIT ? (BR % NW == 0 && NT == 1) : (MT % NW == 0), "bad wave split");
+  static_assert(NTHR % CO == 0, "db accumulation needs a fixed channel per thread");
+  static_assert(!KSPLIT || NW * 1024 <= BR * WOE * CO, "reduction scratch aliases the dZ band");
+  __shared__ float x_s[(BR + 2) * WXP * CI];
+  __shared__ float z_s[BR * WOE * CO];
+  __shared__ float gb_s[NTHR];
+  const int sp = blockIdx.x, r = blockIdx.y;
+  const int count = a.cnt[r];
+  const int j_begin = sp * WGS, j_end = min(count, j_begin + WGS);
+  if (j_begin >= j_end) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 31, kh = lane >> 5;
+  // per-lane operand bases
+  int ab[UMW];
+  int ci0[UMW];
+  float amask = 1.0f;
+#pragma unroll
+  for (int u = 0; u < UMW; ++u) {
+    if (KSPLIT) {
+      const int mm = m < 27 ? m : 0;
+      amask = m < 27 ? 1.0f : 0.0f;
+      const int kyx = mm / 3, c = mm % 3;
+      ab[u] = ((kyx / 3) * WXP + kyx % 3 + kh) * CI + c + wave * RW * WXP * CI;
+      ci0[u] = 0;
+    } else {
+      const int mt = wave + NW * u;
+      const int kyx = mt / (CI / 32);
+      ci0[u] = (mt % (CI / 32)) * 32;
+      ab[u] = ((kyx / 3) * WXP + kyx % 3 + kh) * CI + ci0[u] + m;
+    }
+  }
+  const int zb = kh * CO + m + (KSPLIT ? wave * RW * WOE * CO : 0);
+  floatx16 acc[UMW][NT];
+#pragma unroll
+  for (int u = 0; u < UMW; ++u)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[u][nt] = zero16();
+  float gb = 0.0f;
+  for (int j = j_begin; j < j_end; ++j) {
+    const int64_t slot = (int64_t)r * a.bmax + j;
+    const float* X = a.x_mode == 1 ? a.x + (int64_t)a.idx[slot] * (HI * WI * CI) : a.x + slot * (HI * WI * CI);
+    const float* Z = a.dz + slot * (HO * WO * CO);
+    for (int band = 0; band < NB; ++band) {
+      const int y0 = band * BR;
+      __syncthreads();  // previous band's readers done
+      for (int e = tid; e < (BR + 2) * WXP * CI; e += NTHR) {
+        const int c = e % CI;
+        const int col = (e / CI) % WXP;
+        const int rr = e / (CI * WXP);
+        const int iy = y0 - PAD + rr, ix = col - PAD;
+        x_s[e] = (iy >= 0 && iy < HI && ix >= 0 && ix < WI) ? X[(iy * WI + ix) * CI + c] : 0.0f;
+      }
+      for (int e = tid; e < BR * WOE * CO; e += NTHR) {
+        const int c = e % CO;
+        const int xx = (e / CO) % WOE;
+        const int yy = y0 + e / (CO * WOE);
+        const float v = (yy < HOV && xx < WOV) ? Z[(yy * WO + xx) * CO + c] : 0.0f;
+        z_s[e] = v;
+        gb += v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SW; ++s) {
+        const int yl = (2 * s) / WOE, xl = (2 * s) % WOE;
+        float bz[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bz[nt] = z_s[zb + (yl * WOE + xl) * CO + nt * 32];
+#pragma unroll
+        for (int u = 0; u < UMW; ++u) {
+          float av = x_s[ab[u] + (yl * WXP + xl) * CI];
+          if (KSPLIT) av *= amask;
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[u][nt] = mfma32(av, bz[nt], acc[u][nt]);
+        }
+      }
+    }
+  }
+  float* out = a.wpart + ((int64_t)r * a.splits + sp) * WPART;
+  gb_s[tid] = gb;
+  if (KSPLIT) {
+    __syncthreads();  // all MFMA readers of z_s done: reuse it as the wave-reduction scratch
+    float* red = z_s;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) red[wave * 1024 + acc_row(reg, kh) * 32 + m] = acc[0][0][reg];
+    __syncthreads();
+    for (int e = tid; e < 27 * 32; e += NTHR) {
+      float s = 0.0f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += red[w * 1024 + e];
+      out[a.off_w + e] = s;  // row e/32 = kyx*3 + c, column co: Keras [ky][kx][ci][co] order
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < UMW; ++u) {
+      const int kyx = (wave + NW * u) / (CI / 32);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int ci = ci0[u] + acc_row(reg, kh);
+          out[a.off_w + (kyx * CI + ci) * CO + nt * 32 + m] = acc[u][nt][reg];
+        }
+    }
+    __syncthreads();
+  }
+  if (tid < CO) {
+    float s = 0.0f;
+    for (int i = 0; i < NTHR / CO; ++i) s += gb_s[tid + CO * i];
+    out[a.off_b + tid] = s;
+  }
+}
+
+// RMSprop on W1..b4 (params [0, OFF_W5)) from the split partials, splits summed in order.
+__device__ __forceinline__ bool small_param(int e) {
+  return (e < OFF_W1 + 864) || (e >= OFF_B1 && e < OFF_B1 + 32) || (e >= OFF_W2 && e < OFF_B2 + 32) ||
+         (e >= OFF_W3 && e < OFF_B3 + 64) || (e >= OFF_W4 && e < OFF_B4 + 64);
+}
+
+__global__ void rmsprop_small_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int splits,
+                                     const float* __restrict__ wpart, float* __restrict__ params,
+                                     float* __restrict__ rms, float lr, float rho, float omr, float decay, float eps) {
+  const int r = blockIdx.y;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= OFF_W5 || !small_param(e)) return;
+  const float* w = wpart + (int64_t)r * splits * WPART + e;
+  const int used = (count + WGS - 1) / WGS;
+  float g = 0.0f;
+  for (int s = 0; s < used; ++s) g += w[(int64_t)s * WPART];
+  const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
+  const int64_t o = (int64_t)r * STRIDE + e;
+  rms_apply(params[o], rms[o], g, cfg);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense(512) + ReLU (+ dropout .5 when training): H[slot][n] = relu(sum_k D4[slot][k] W5[k][n] + b5[n]).
+// Block = 32 samples x 128 columns (4 waves x 32); A staged in LDS, W5 streamed.
+// ------------------------------------------------------------------------------------------------
+constexpr int DF_K = 64;
+
+__global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict__ A, const int32_t* __restrict__ cnt,
+                                                         int cnt_all, int bmax, const float* __restrict__ params,
+                                                         int64_t stride, const uint64_t* __restrict__ drop_key,
+                                                         float* __restrict__ H, uint8_t* __restrict__ code) {
+  __shared__ float a_s[32 * (DF_K + 1)];
+  const int r = blockIdx.z;
+  const int m0 = blockIdx.x * 32;
+  const int count = cnt ? cnt[r] : cnt_all;
+  if (m0 >= count) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.y * 128 + wave * 32;
+  const int kh = lane >> 5;
+  const float* Ar = A + (int64_t)r * bmax * FEAT;
+  const float* W = params + (int64_t)r * stride + OFF_W5;
+  floatx16 acc = zero16();
+  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
+    for (int e = tid; e < 32 * DF_K; e += 256) {
+      const int mm = e / DF_K, kk = e % DF_K;
+      a_s[mm * (DF_K + 1) + kk] = (m0 + mm < count) ? Ar[(int64_t)(m0 + mm) * FEAT + k0 + kk] : 0.0f;
+    }
+    __syncthreads();
+    const float* Wk = W + (int64_t)k0 * HID + n0 + (lane & 31);
+#pragma unroll 8
+    for (int s = 0; s < DF_K / 2; ++s) {
+      const float av = a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh];
+      const float b = Wk[(int64_t)(2 * s + kh) * HID];
+      acc = mfma32(av, b, acc);
+    }
+    __syncthreads();
+  }
+  const int col = n0 + (lane & 31);
+  const float bias = params[(int64_t)r * stride + OFF_B5 + col];
+  const uint64_t dkey = drop_key ? drop_key[r] : 0ull;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = m0 + acc_row(reg, kh);
+    if (row < count) {
+      const float z = acc[reg] + bias;
+      const float h = fmaxf(z, 0.0f);
+      const int64_t o = ((int64_t)r * bmax + row) * HID + col;
+      if (drop_key) {
+        const bool keep = drop_keep(dkey, DROP_L5, (uint32_t)row, (uint32_t)col, THR_50);
+        H[o] = keep ? h * SCALE_50 : 0.0f;
+        code[o] = (uint8_t)((keep ? CODE_KEEP : 0) | (z > 0.0f ? CODE_POS : 0));
+      } else {
+        H[o] = h;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Head: Dense(10) + softmax-CE gradient (mean over the batch), dW6/db6 + RMSprop, dh5 through dropout'
+// and relu'.  One block per replica.
+// ------------------------------------------------------------------------------------------------
+constexpr int HEAD_CHUNK = 256;
+constexpr int W6N = HID * NCLS + NCLS;  // W6 and b6 are contiguous
+constexpr int HEAD_G = (W6N + 255) / 256;
+
+__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5, const uint8_t* __restrict__ code5,
+                                                   const int32_t* __restrict__ idx, const int32_t* __restrict__ labels,
+                                                   const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t,
+                                                   int bmax, float* __restrict__ params, float* __restrict__ rms,
+                                                   float* __restrict__ dH, float lr, float rho, float omr,
+                                                   float decay, float eps) {
+  __shared__ float w6_s[W6N];
+  __shared__ float dl_s[HEAD_CHUNK * NCLS];
+  const int r = blockIdx.x;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  float* P = params + (int64_t)r * STRIDE;
+  for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
+  __syncthreads();
+  const float inv_b = 1.0f / (float)count;
+  float gacc[HEAD_G];
+#pragma unroll
+  for (int u = 0; u < HEAD_G; ++u) gacc[u] = 0.0f;
+  const float* Dr = D5 + (int64_t)r * bmax * HID;
+  for (int c0 = 0; c0 < count; c0 += HEAD_CHUNK) {
+    const int cn = min(HEAD_CHUNK, count - c0);
+    if (tid < cn) {
+      const int jj = c0 + tid;
+      const float* h = Dr + (int64_t)jj * HID;
+      float z[NCLS];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
+      for (int c = 0; c < HID; ++c) {
+        const float hv = h[c];
+#pragma unroll
+        for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
+      }
+      float mx = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o) mx = fmaxf(mx, z[o]);
+      float s = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) { z[o] = expf(z[o] - mx); s += z[o]; }
+      const int y = labels[idx[(int64_t)r * bmax + jj]];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) dl_s[tid * NCLS + o] = (z[o] / s - (o == y ? 1.0f : 0.0f)) * inv_b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < HEAD_G; ++u) {
+      const int e = tid + 256 * u;
+      if (e < HID * NCLS) {
+        const int c = e / NCLS, o = e % NCLS;
+        float acc = 0.0f;
+        for (int jj = 0; jj < cn; ++jj) acc += Dr[(int64_t)(c0 + jj) * HID + c] * dl_s[jj * NCLS + o];
+        gacc[u] += acc;
+      } else if (e < W6N) {
+        const int o = e - HID * NCLS;
+        float acc = 0.0f;
+        for (int jj = 0; jj < cn; ++jj) acc += dl_s[jj * NCLS + o];
+        gacc[u] += acc;
+      }
+    }
+    const uint8_t* cd = code5 + (int64_t)r * bmax * HID;
+    for (int e = tid; e < cn * HID; e += 256) {
+      const int jj = e / HID, c = e % HID;
+      float acc = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) acc += dl_s[jj * NCLS + o] * w6_s[c * NCLS + o];
+      const uint32_t k = cd[(int64_t)(c0 + jj) * HID + c];
+      dH[((int64_t)r * bmax + c0 + jj) * HID + c] =
+          ((k & CODE_KEEP) && (k & CODE_POS)) ? acc * SCALE_50 : 0.0f;
+    }
+    __syncthreads();
+  }
+  const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
+  float* Rr = rms + (int64_t)r * STRIDE;
+#pragma unroll
+  for (int u = 0; u < HEAD_G; ++u) {
+    const int e = tid + 256 * u;
+    if (e < W6N) {
+      const int64_t o = OFF_W6 + e;
+      float p = P[o], aa = Rr[o];
+      rms_apply(p, aa, gacc[u], cfg);
+      P[o] = p;
+      Rr[o] = aa;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense(512) backward + RMSprop, per 16-row slice of W5 (16 threads per row, 8 fvec4 each):
+//   dd4[j][k] = sum_n dh5[j][n] W5[k][n];  dW5[k][n] = sum_j d4[j][k] dh5[j][n];  db5 (slice-0 block).
+// dd4 goes through dropout'(.25) and the 2x2 pool (argmax + relu' from code4) into the dense dz4.
+// ------------------------------------------------------------------------------------------------
+constexpr int D5_ROWS = 16;
+constexpr int D5_SCHUNK = 16;
+
+__global__ __launch_bounds__(256) void dense5_bwd_kernel(
+    const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
+    float* __restrict__ rms, float* __restrict__ dZ4, float lr, float rho, float omr, float decay, float eps) {
+  __shared__ fvec4 dh_s[D5_SCHUNK * (HID / 4)];
+  __shared__ float p_s[D5_SCHUNK * D5_ROWS];
+  const int r = blockIdx.y;
+  const int k0 = blockIdx.x * D5_ROWS;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  const int rowl = tid >> 4;
+  const int c16 = tid & 15;
+  const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
+  const int64_t roff = (int64_t)r * STRIDE + OFF_W5 + (int64_t)(k0 + rowl) * HID;
+  fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c16;
+  fvec4* Ra = reinterpret_cast<fvec4*>(rms + roff) + c16;
+  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  fvec4 w[8], g[8], av[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w[i] = W[16 * i];
+    g[i] = z4;
+    av[i] = z4;
+  }
+  if (!cfg.reset) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) av[i] = __builtin_nontemporal_load(Ra + 16 * i);
+  }
+  const int k = k0 + rowl;
+  const int pix = k / 64, ch = k % 64;
+  const int py = pix / 6, px = pix % 6;
+  const float* Pr = D4 + (int64_t)r * bmax * FEAT;
+  const fvec4* dHr = reinterpret_cast<const fvec4*>(dH + (int64_t)r * bmax * HID);
+  for (int c0 = 0; c0 < count; c0 += D5_SCHUNK) {
+    const int cn = min(D5_SCHUNK, count - c0);
+    for (int e = tid; e < cn * (HID / 4); e += 256) dh_s[e] = dHr[(int64_t)c0 * (HID / 4) + e];
+    for (int e = tid; e < cn * D5_ROWS; e += 256) {
+      const int jj = e / D5_ROWS, kk = e % D5_ROWS;
+      p_s[e] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + kk];
+    }
+    __syncthreads();
+    for (int jj = 0; jj < cn; ++jj) {
+      const float pv = p_s[jj * D5_ROWS + rowl];
+      float d = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const fvec4 dh = dh_s[jj * (HID / 4) + c16 + 16 * i];
+        g[i].x += pv * dh.x; g[i].y += pv * dh.y; g[i].z += pv * dh.z; g[i].w += pv * dh.w;
+        d += dh.x * w[i].x; d += dh.y * w[i].y; d += dh.z * w[i].z; d += dh.w * w[i].w;
+      }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 8, 64);
+      if (c16 < 4) {  // un-pool: lane c16 = q writes window pixel q
+        const int64_t slot = (int64_t)r * bmax + c0 + jj;
+        const uint32_t c = code4[slot * FEAT + k];
+        const float v = (c & CODE_KEEP) ? d * SCALE_25 : 0.0f;
+        const bool hit = (c & CODE_POS) && (int)(c & 3) == c16;
+        dZ4[slot * MPLC_CIFAR_DZ4 + ((2 * py + (c16 >> 1)) * 13 + 2 * px + (c16 & 1)) * 64 + ch] = hit ? v : 0.0f;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fvec4 pw = w[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float p1 = pw[q], a1 = av[i][q];
+      rms_apply(p1, a1, g[i][q], cfg);
+      pw[q] = p1;
+      av[i][q] = a1;
+    }
+    W[16 * i] = pw;
+    __builtin_nontemporal_store(av[i], Ra + 16 * i);
+  }
+  if (blockIdx.x == 0) {
+    const float* dHs = dH + (int64_t)r * bmax * HID;
+    for (int c = tid; c < HID; c += 256) {
+      float gb = 0.0f;
+      for (int jj = 0; jj < count; ++jj) gb += dHs[(int64_t)jj * HID + c];
+      const int64_t o = (int64_t)r * STRIDE + OFF_B5 + c;
+      rms_apply(params[o], rms[o], gb, cfg);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Evaluation head: logits, accuracy count and summed cross-entropy per model (deterministic order).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict__ H, int count, int chunk,
+                                                        const int32_t* __restrict__ labels, int row_base,
+                                                        const float* __restrict__ params, int64_t stride,
+                                                        int32_t* __restrict__ correct, double* __restrict__ loss_sum) {
+  __shared__ float w6_s[W6N];
+  __shared__ double ls[256];
+  __shared__ int cs[256];
+  const int mdl = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* P = params + (int64_t)mdl * stride;
+  for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
+  __syncthreads();
+  double lsum = 0.0;
+  int csum = 0;
+  for (int jj = tid; jj < count; jj += 256) {
+    const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
+    float z[NCLS];
+#pragma unroll
+    for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
+    for (int c = 0; c < HID; ++c) {
+      const float hv = h[c];
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
+    }
+    int am = 0;
+    float mx = z[0];
+#pragma unroll
+    for (int o = 1; o < NCLS; ++o)
+      if (z[o] > mx) { mx = z[o]; am = o; }
+    float s = 0.0f;
+#pragma unroll
+    for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
+    const int y = labels[row_base + jj];
+    lsum += (double)(logf(s) + mx - z[y]);
+    csum += (am == y) ? 1 : 0;
+  }
+  ls[tid] = lsum;
+  cs[tid] = csum;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if (tid < off) { ls[tid] += ls[tid + off]; cs[tid] += cs[tid + off]; }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    correct[mdl] += cs[0];
+    loss_sum[mdl] += ls[0];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// layer instantiations: <HI, WI, CI, CO, PAD, BR, NW, UM, EPI> (conv) and <HI, WI, CI, CO, PAD, HOV, WOV,
+// BR, NW> (wgrad); geometry checked by static_asserts, LDS per block in the comment
+// ------------------------------------------------------------------------------------------------
+#define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
+#define CONV2_FWD conv_kernel<32, 32, 32, 32, 0, 5, 5, 2, EPI_FWD_POOL>    /* 3 bands, 50.7 KB */
+#define CONV3_FWD conv_kernel<15, 15, 32, 64, 1, 15, 4, 2, EPI_FWD>        /* 1 band,  38.1 KB */
+#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 5, 1, EPI_FWD_POOL>    /* 1 band,  54.6 KB */
+#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 8, 4, 1, EPI_BWD_MASK>  /* 2 bands, 44.2 KB */
+#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 8, 4, 1, EPI_BWD_UNPOOL>/* 2 bands, 44.2 KB */
+#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 8, 4, 2, EPI_BWD_MASK>  /* 4 bands, 44.9 KB */
+#define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
+#define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 5, 3>
+#define CONV3_WGRAD wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 5, 3>
+#define CONV4_WGRAD wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 6>
+
+inline int launch_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MPLC_OK : (int)e;
+}
+
+ConvArgs conv_args(const float* in, int in_mode, int row_base, const int32_t* idx, const int32_t* cnt, int cnt_all,
+                   int bmax, const float* w, int64_t w_rstride) {
+  ConvArgs a{};
+  a.in = in;
+  a.in_mode = in_mode;
+  a.row_base = row_base;
+  a.idx = idx;
+  a.cnt = cnt;
+  a.cnt_all = cnt_all;
+  a.bmax = bmax;
+  a.w = w;
+  a.w_rstride = w_rstride;
+  return a;
+}
+
+// forward of conv1..dense5 for R models x B slots (train: dropout + codes; eval: inference)
+void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, int row_base, const int32_t* idx,
+                     const int32_t* cnt, int cnt_all, const float* params, int64_t stride, const uint64_t* drop_key,
+                     float* a1, float* d2, uint8_t* code2, float* a3, float* d4, uint8_t* code4, float* h5,
+                     uint8_t* code5, int prof, void* pb, void* pe) {
+#define PB(k) \
+  if (prof == (k) && pb) (void)hipEventRecord((hipEvent_t)pb, s)
+#define PE(k) \
+  if (prof == (k) && pe) (void)hipEventRecord((hipEvent_t)pe, s)
+  ConvArgs c1 = conv_args(x, in_mode, row_base, idx, cnt, cnt_all, B, params + OFF_W1, stride);
+  c1.bias = params + OFF_B1;
+  c1.b_rstride = stride;
+  c1.out = a1;
+  PB(1);
+  CONV1_FWD<<<dim3(4, B, R), 256, 0, s>>>(c1);
+  PE(1);
+  ConvArgs c2 = conv_args(a1, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W2, stride);
+  c2.bias = params + OFF_B2;
+  c2.b_rstride = stride;
+  c2.drop_key = drop_key;
+  c2.drop_layer = DROP_L2;
+  c2.out = d2;
+  c2.code_out = code2;
+  PB(2);
+  CONV2_FWD<<<dim3(3, B, R), 320, 0, s>>>(c2);
+  PE(2);
+  ConvArgs c3 = conv_args(d2, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W3, stride);
+  c3.bias = params + OFF_B3;
+  c3.b_rstride = stride;
+  c3.out = a3;
+  PB(3);
+  CONV3_FWD<<<dim3(1, B, R), 256, 0, s>>>(c3);
+  PE(3);
+  ConvArgs c4 = conv_args(a3, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W4, stride);
+  c4.bias = params + OFF_B4;
+  c4.b_rstride = stride;
+  c4.drop_key = drop_key;
+  c4.drop_layer = DROP_L4;
+  c4.out = d4;
+  c4.code_out = code4;
+  PB(4);
+  CONV4_FWD<<<dim3(1, B, R), 320, 0, s>>>(c4);
+  PE(4);
+  PB(5);
+  dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, drop_key,
+                                                                      h5, code5);
+  PE(5);
+#undef PB
+#undef PE
+}
+
+}  // namespace
+
+extern "C" {
+
+int mplc_cifar_stride(void) { return MPLC_CIFAR_STRIDE; }
+
+int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
+  if (!params || !keys || n_models < 1 || n_models > 65535 || stride != MPLC_CIFAR_STRIDE) return MPLC_E_ARG;
+  init_params_kernel<<<dim3(512, n_models), 256, 0, (hipStream_t)stream>>>(params, stride, keys);
+  return launch_status();
+}
+
+#define PROF_BEGIN(k) \
+  if (t->prof_kernel == (k) && t->prof_begin) (void)hipEventRecord((hipEvent_t)t->prof_begin, s)
+#define PROF_END(k) \
+  if (t->prof_kernel == (k) && t->prof_end) (void)hipEventRecord((hipEvent_t)t->prof_end, s)
+
+int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
+  if (!t || t->n_rep < 1 || t->n_rep > 65535 || t->bmax < 1 || t->bmax > 65535) return MPLC_E_ARG;
+  if (t->wg_splits != (t->bmax + WGS - 1) / WGS) return MPLC_E_SHAPE;
+  if (!t->reps || !t->rows || !t->splits || !t->x || !t->labels || !t->params || !t->rms || !t->idx || !t->cnt ||
+      !t->opt_t || !t->drop_key || !t->a1 || !t->d2 || !t->code2 || !t->a3 || !t->d4 || !t->code4 || !t->d5 ||
+      !t->code5 || !t->dh5 || !t->dz4 || !t->dz3 || !t->dz2 || !t->dz1 || !t->wt || !t->wpart)
+    return MPLC_E_ARG;
+  if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int R = t->n_rep, B = t->bmax;
+  const int64_t slots = (int64_t)R * B;
+  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->step,
+                                                                   t->minibatch_count, t->round_len, t->epochs,
+                                                                   t->idx, t->cnt, t->opt_t, t->drop_key);
+  enqueue_forward(s, R, B, t->x, 1, 0, t->idx, t->cnt, 0, t->params, STRIDE, t->drop_key, t->a1, t->d2, t->code2,
+                  t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end);
+  PROF_BEGIN(6);
+  head_kernel<<<R, 256, 0, s>>>(t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5,
+                                t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
+  PROF_END(6);
+  PROF_BEGIN(7);
+  dense5_bwd_kernel<<<dim3(FEAT / D5_ROWS, R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
+                                                            t->rms, t->dz4, t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
+  PROF_END(7);
+  transpose_w_kernel<<<dim3(32, R), 256, 0, s>>>(t->params, t->cnt, t->wt);
+  const int SP = t->wg_splits;
+  WgArgs w4{t->a3, 0, t->idx, t->cnt, B, SP, t->dz4, t->wpart, (int)OFF_W4, (int)OFF_B4};
+  PROF_BEGIN(8);
+  CONV4_WGRAD<<<dim3(SP, R), 384, 0, s>>>(w4);
+  PROF_END(8);
+  ConvArgs g4 = conv_args(t->dz4, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W4, MPLC_CIFAR_WT);
+  g4.aux = t->a3;
+  g4.out = t->dz3;
+  PROF_BEGIN(9);
+  CONV4_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g4);
+  PROF_END(9);
+  WgArgs w3{t->d2, 0, t->idx, t->cnt, B, SP, t->dz3, t->wpart, (int)OFF_W3, (int)OFF_B3};
+  PROF_BEGIN(10);
+  CONV3_WGRAD<<<dim3(SP, R), 192, 0, s>>>(w3);
+  PROF_END(10);
+  ConvArgs g3 = conv_args(t->dz3, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W3, MPLC_CIFAR_WT);
+  g3.code_in = t->code2;
+  g3.out = t->dz2;
+  PROF_BEGIN(11);
+  CONV3_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g3);
+  PROF_END(11);
+  WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2};
+  PROF_BEGIN(12);
+  CONV2_WGRAD<<<dim3(SP, R), 192, 0, s>>>(w2);
+  PROF_END(12);
+  ConvArgs g2 = conv_args(t->dz2, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W2, MPLC_CIFAR_WT);
+  g2.aux = t->a1;
+  g2.out = t->dz1;
+  PROF_BEGIN(13);
+  CONV2_DGRAD<<<dim3(4, B, R), 256, 0, s>>>(g2);
+  PROF_END(13);
+  WgArgs w1{t->x, 1, t->idx, t->cnt, B, SP, t->dz1, t->wpart, (int)OFF_W1, (int)OFF_B1};
+  PROF_BEGIN(14);
+  CONV1_WGRAD<<<dim3(SP, R), 256, 0, s>>>(w1);
+  PROF_END(14);
+  PROF_BEGIN(15);
+  rmsprop_small_kernel<<<dim3((OFF_W5 + 255) / 256, R), 256, 0, s>>>(t->cnt, t->opt_t, SP, t->wpart, t->params,
+                                                                      t->rms, t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
+  PROF_END(15);
+  return launch_status();
+}
+
+int64_t mplc_cifar_eval_workspace_floats(int n_models, int chunk) {
+  return (int64_t)n_models * chunk * (MPLC_CIFAR_A1 + MPLC_CIFAR_D2 + MPLC_CIFAR_A3 + MPLC_CIFAR_D4 + MPLC_CIFAR_H5);
+}
+
+int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
+                        int n_samples, int chunk, float* ws, int32_t* correct, double* loss_sum, void* stream) {
+  if (!params || !x || !labels || !ws || !correct || !loss_sum) return MPLC_E_ARG;
+  if (n_models < 1 || n_models > 65535 || n_samples < 1 || chunk < 1 || chunk > 65535 || stride != MPLC_CIFAR_STRIDE)
+    return MPLC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t mc = (int64_t)n_models * chunk;
+  float* a1 = ws;
+  float* d2 = a1 + mc * MPLC_CIFAR_A1;
+  float* a3 = d2 + mc * MPLC_CIFAR_D2;
+  float* d4 = a3 + mc * MPLC_CIFAR_A3;
+  float* h5 = d4 + mc * MPLC_CIFAR_D4;
+  for (int s0 = 0; s0 < n_samples; s0 += chunk) {
+    const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
+    enqueue_forward(s, n_models, chunk, x, 2, s0, nullptr, nullptr, cn, params, stride, nullptr, a1, d2, nullptr, a3,
+                    d4, nullptr, h5, nullptr, 0, nullptr, nullptr);
+    eval_head_kernel<<<n_models, 256, 0, s>>>(h5, cn, chunk, labels, s0, params, stride, correct, loss_sum);
+    const int st = launch_status();
+    if (st) return st;
+  }
+  return MPLC_OK;
+}
+
+}  // extern "C"

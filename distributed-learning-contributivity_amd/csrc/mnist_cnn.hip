@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "mplc_hip.h"
+#include "keyed.h"
 
 namespace {
 
@@ -81,40 +82,6 @@ __device__ __forceinline__ floatx16 conv1_mfma(const float* img_s, int pix, int 
 __device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
 
 // ------------------------------------------------------------------------------------------------
-// Keyed index permutations (bit-identical restatement in oracle/cnn.py)
-// ------------------------------------------------------------------------------------------------
-__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ uint64_t subkey(uint64_t key, uint32_t a, uint32_t b) {
-  return mix64(key ^ mix64(((uint64_t)a << 32) | (uint64_t)b));
-}
-
-// Bijection of [0, n) (balanced 4-round Feistel on 2h bits + cycle walking).
-__device__ __forceinline__ uint32_t keyed_perm(uint64_t key, uint32_t n, uint32_t i) {
-  if (n <= 1) return 0;
-  int bits = 32 - __clz(n - 1);  // ceil(log2 n)
-  const int h = (bits + 1) >> 1;
-  const uint32_t mask = (1u << h) - 1u;
-  uint32_t x = i;
-  do {
-    uint32_t L = x >> h, R = x & mask;
-#pragma unroll
-    for (int rd = 0; rd < 4; ++rd) {
-      const uint32_t F = (uint32_t)mix64(key ^ ((uint64_t)rd << 40) ^ (uint64_t)R) & mask;
-      const uint32_t nl = R;
-      R = L ^ F;
-      L = nl;
-    }
-    x = (L << h) | R;
-  } while (x >= n);
-  return x;
-}
-
-// ------------------------------------------------------------------------------------------------
 // Initialisation: glorot_uniform kernels (Keras default), zero biases / padding.
 // u = top 24 bits of mix64(key + i*golden) / 2^24;  w = (2u - 1) * limit  (fp32, exact restatable)
 // ------------------------------------------------------------------------------------------------
@@ -160,46 +127,8 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
   if (gid >= (int64_t)n_rep * bmax) return;
   const int r = (int)(gid / bmax);
   const int j = (int)(gid % bmax);
-  const mplc_replica_t rep = reps[r];
-  int c = 0, at = 0, row = -1;
-  if (rep.kind == MPLC_REP_FEDAVG) {
-    const int per_epoch = M * round_len;
-    const int e = step / per_epoch;
-    const int rem = step % per_epoch;
-    const int m = rem / round_len;
-    const int t = rem % round_len;
-    if (e < epochs) {
-      const int s0 = splits[rep.split_off + m];
-      const int s1 = splits[rep.split_off + m + 1];
-      const int L = s1 - s0;
-      const int nsteps = (L + rep.batch - 1) / rep.batch;
-      if (t < nsteps) {
-        c = min(rep.batch, L - t * rep.batch);
-        at = t + 1;
-        if (j < c) {
-          // Keras fit shuffle inside minibatch m, then the epoch permutation of split_minibatches
-          const uint32_t q = keyed_perm(subkey(rep.key, 0x20000u + (uint32_t)e, (uint32_t)m), (uint32_t)L,
-                                        (uint32_t)(t * rep.batch + j));
-          const uint32_t pos = keyed_perm(subkey(rep.key, 0x10000u + (uint32_t)e, 0u), (uint32_t)rep.n_rows,
-                                          (uint32_t)s0 + q);
-          row = rows[rep.rows_off + (int)pos];
-        }
-      }
-    }
-  } else if (rep.kind == MPLC_REP_SINGLE) {
-    const int spe = (rep.n_rows + rep.batch - 1) / rep.batch;
-    const int e = step / spe;
-    const int t = step % spe;
-    if (e < epochs) {
-      c = min(rep.batch, rep.n_rows - t * rep.batch);
-      at = step + 1;
-      if (j < c) {
-        const uint32_t pos = keyed_perm(subkey(rep.key, 0x30000u + (uint32_t)e, 0u), (uint32_t)rep.n_rows,
-                                        (uint32_t)(t * rep.batch + j));
-        row = rows[rep.rows_off + (int)pos];
-      }
-    }
-  }
+  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits);
+  const int c = ss.c, at = ss.at, row = ss.row;
   idx[gid] = row;
   if (j == 0) {
     cnt[r] = c;

@@ -1,0 +1,137 @@
+"""Host hooks of the batched CIFAR10 CNN trainer (csrc/cifar_cnn.hip, include/mplc_hip_cifar.h).
+
+Architecture and optimizer of the reference's Cifar10.generate_new_model (mplc/dataset.py:167-200):
+Conv(32,same) Conv(32) Pool Dropout(.25) Conv(64,same) Conv(64) Pool Dropout(.25) Dense(512) Dropout(.5)
+Dense(10); categorical CE; RMSprop(learning_rate=1e-4, decay=1e-6) with Keras 2.3.1 defaults rho=0.9,
+epsilon=1e-7.  The coalition orchestration (FedAvg rounds with a fresh optimizer per partner fit,
+singletons with a persistent one, early stopping, test accuracy) is the model-independent TrainBatch /
+CnnBatchTrainer of mplc/cnn.py; this module provides the CIFAR parameter layout, state and launches.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+STRIDE = 1251008
+NPARAM = 1250954
+WG_SAMPLES = 4
+A1, D2, A3, D4, H5 = 32768, 7200, 14400, 2304, 512
+DZ4, DZ3, DZ2, DZ1 = 10816, 14400, 28800, 32768
+WT, WPART = 64512, 65664
+EVAL_FLOATS = A1 + D2 + A3 + D4 + H5  # per model per evaluated sample
+
+KERNEL_IDS = {"conv1_fwd": 1, "conv2_fwd": 2, "conv3_fwd": 3, "conv4_fwd": 4, "dense5_fwd": 5, "head": 6,
+              "dense5_bwd": 7, "conv4_wgrad": 8, "conv4_dgrad": 9, "conv3_wgrad": 10, "conv3_dgrad": 11,
+              "conv2_wgrad": 12, "conv2_dgrad": 13, "conv1_wgrad": 14, "rmsprop_small": 15}
+# algorithmic FLOPs per sample of each profiled launch (bench roofline)
+FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 900 * 32 * 288 * 2, "conv3_fwd": 225 * 64 * 288 * 2,
+                   "conv4_fwd": 144 * 64 * 576 * 2, "conv4_dgrad": 144 * 64 * 576 * 2,
+                   "conv3_dgrad": 225 * 32 * 576 * 2, "conv2_dgrad": 900 * 32 * 288 * 2,
+                   "conv4_wgrad": 144 * 64 * 576 * 2, "conv3_wgrad": 225 * 64 * 288 * 2,
+                   "conv2_wgrad": 900 * 32 * 288 * 2, "conv1_wgrad": 1024 * 32 * 27 * 2}
+
+
+class CifarTrainT(ctypes.Structure):
+    _fields_ = ([("n_rep", ctypes.c_int32), ("bmax", ctypes.c_int32), ("wg_splits", ctypes.c_int32),
+                 ("pad0", ctypes.c_int32), ("step", ctypes.c_int32), ("minibatch_count", ctypes.c_int32),
+                 ("round_len", ctypes.c_int32), ("epochs", ctypes.c_int32)]
+                + [(n, ctypes.c_void_p) for n in ("reps", "rows", "splits", "x", "labels", "params", "rms", "idx",
+                                                   "cnt", "opt_t", "drop_key", "a1", "d2", "code2", "a3", "d4",
+                                                   "code4", "d5", "code5", "dh5", "dz4", "dz3", "dz2", "dz1", "wt",
+                                                   "wpart")]
+                + [(n, ctypes.c_float) for n in ("lr", "rho", "one_minus_rho", "decay", "eps")]
+                + [("prof_kernel", ctypes.c_int32), ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p)])
+
+
+_BOUND = False
+
+
+def _bind():
+    global _BOUND
+    if _BOUND:
+        return
+    _native.register("mplc_cifar_train_step", ctypes.c_int, [ctypes.POINTER(CifarTrainT), ctypes.c_void_p])
+    lib = _native.lib()
+    if lib.mplc_cifar_stride() != STRIDE:
+        raise RuntimeError("libmplc_hip.so CIFAR layout mismatch; rebuild")
+    _BOUND = True
+
+
+class CifarModel:
+    """Model hooks (see mplc.cnn.MnistModel) for the CIFAR10 CNN."""
+    name = "cifar10_cnn"
+    STRIDE, NPARAM = STRIDE, NPARAM
+    KERNEL_IDS = KERNEL_IDS
+    input_shape = (32, 32, 3)
+    # Keras 2.3.1 RMSprop(learning_rate=0.0001, decay=1e-6): rho 0.9, epsilon K.epsilon() = 1e-7
+    lr, rho, decay, eps = 1e-4, 0.9, 1e-6, 1e-7
+
+    def __init__(self):
+        _bind()
+        self.lib = _native.lib()
+
+    def replica_bytes(self, bmax):
+        slot = 4 * (A1 + D2 + A3 + D4 + 2 * H5 + DZ4 + DZ3 + DZ2 + DZ1) + (D2 + D4 + H5) + 4
+        splits = (bmax + WG_SAMPLES - 1) // WG_SAMPLES
+        return 2 * STRIDE * 4 + bmax * slot + WT * 4 + splits * WPART * 4 + 24
+
+    def init_params(self, glob, keys, stream):
+        _native.check(self.lib.mplc_cifar_init_params(_native.ptr(glob), STRIDE, _native.ptr(keys), glob.shape[0],
+                                                      stream), "mplc_cifar_init_params")
+
+    def alloc(self, st):
+        import torch
+        eng, dev, R, B = st.eng, st.dev, st.R, st.bmax
+        f32 = dict(dtype=torch.float32, device=dev)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        splits = (B + WG_SAMPLES - 1) // WG_SAMPLES
+        st.rms = torch.zeros((R, STRIDE), **f32)
+        st.ws = dict(
+            idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), opt_t=torch.empty(R, **i32),
+            drop_key=torch.empty(R, dtype=torch.int64, device=dev),
+            a1=torch.empty((R, B, A1), **f32), d2=torch.empty((R, B, D2), **f32), code2=torch.empty((R, B, D2), **u8),
+            a3=torch.empty((R, B, A3), **f32), d4=torch.empty((R, B, D4), **f32), code4=torch.empty((R, B, D4), **u8),
+            d5=torch.empty((R, B, H5), **f32), code5=torch.empty((R, B, H5), **u8), dh5=torch.empty((R, B, H5), **f32),
+            dz4=torch.zeros((R, B, DZ4), **f32), dz3=torch.empty((R, B, DZ3), **f32),
+            dz2=torch.empty((R, B, DZ2), **f32), dz1=torch.empty((R, B, DZ1), **f32),
+            wt=torch.empty((R, WT), **f32), wpart=torch.empty((R, splits, WPART), **f32))
+        t = CifarTrainT()
+        t.n_rep, t.bmax, t.wg_splits = R, B, splits
+        t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
+        t.reps, t.rows, t.splits = st.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
+        t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
+        t.params, t.rms = st.params.data_ptr(), st.rms.data_ptr()
+        for k, v in st.ws.items():
+            setattr(t, k, v.data_ptr())
+        t.lr, t.rho, t.decay, t.eps = self.lr, self.rho, self.decay, self.eps
+        t.one_minus_rho = float(np.float32(1.0 - self.rho))  # Keras: (1. - rho) on the Python double
+        st.t = t
+
+    def free(self, st):
+        st.rms = None
+
+    def step(self, st, s, prof):
+        st.t.step = s
+        if prof is not None:
+            ev0, ev1 = prof.pair()
+            st.t.prof_kernel = self.KERNEL_IDS[prof.kernel]
+            st.t.prof_begin, st.t.prof_end = ev0, ev1
+        _native.check(self.lib.mplc_cifar_train_step(ctypes.byref(st.t), st.stream), "mplc_cifar_train_step")
+
+    def evaluate(self, eng, sel, x, y):
+        import torch
+        dev = eng.device
+        stream = _native.stream_handle(dev)
+        n = int(y.numel())
+        C = sel.shape[0]
+        chunk = int(max(16, min(n, eng.eval_budget_bytes // max(1, C * EVAL_FLOATS * 4))))
+        chunk = min(chunk, 65535)
+        ws = torch.empty(int(self.lib.mplc_cifar_eval_workspace_floats(C, chunk)), dtype=torch.float32, device=dev)
+        correct = torch.zeros(C, dtype=torch.int32, device=dev)
+        loss = torch.zeros(C, dtype=torch.float64, device=dev)
+        _native.check(self.lib.mplc_cifar_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n,
+                                                   chunk, _native.ptr(ws), _native.ptr(correct), _native.ptr(loss),
+                                                   stream), "mplc_cifar_evaluate")
+        return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n

@@ -109,12 +109,90 @@ def minibatch_bounds(n, M):
     return [0] + [int(v) for v in inner] + [int(n)]
 
 
+class MnistModel:
+    """Model hooks of the batched MNIST CNN (csrc/mnist_cnn.hip): parameter layout, optimizer state,
+    workspaces, one lockstep step, evaluation.  TrainBatch / CnnBatchTrainer drive any model with these."""
+    name = "mnist_cnn"
+    STRIDE, NPARAM = STRIDE, NPARAM
+    KERNEL_IDS = KERNEL_IDS
+    input_shape = (28, 28)
+
+    def __init__(self):
+        _bind()
+        self.lib = _native.lib()
+
+    def replica_bytes(self, bmax):
+        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + 2 * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
+                + 9 * 64 * 32 * 4 + bmax * 12)
+
+    def init_params(self, glob, keys, stream):
+        _native.check(self.lib.mplc_cnn_init_params(_native.ptr(glob), STRIDE, _native.ptr(keys), glob.shape[0], stream),
+                      "mplc_cnn_init_params")
+
+    def alloc(self, st):
+        """Optimizer state, workspaces and the step struct of a TrainBatch (params already set)."""
+        import torch
+        eng, dev, R, B = st.eng, st.dev, st.R, st.bmax
+        f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        st.adam_m = torch.zeros((R, STRIDE), **f32)
+        st.adam_v = torch.zeros((R, STRIDE), **f32)
+        splits = (B + WG_SAMPLES - 1) // WG_SAMPLES
+        st.ws = dict(
+            idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
+            pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
+            hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
+            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, 2, W1P), **f32),
+            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, 9 * 64 * 32), **f32))
+        t = TrainT()
+        t.n_rep, t.bmax, t.w2_splits = R, B, splits
+        t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
+        t.reps, t.rows, t.splits = st.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
+        t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
+        t.params, t.adam_m, t.adam_v = st.params.data_ptr(), st.adam_m.data_ptr(), st.adam_v.data_ptr()
+        for k, v in st.ws.items():
+            setattr(t, k, v.data_ptr())
+        t.lr, t.beta1, t.beta2, t.eps = 0.001, 0.9, 0.999, 1e-7
+        st.t = t
+
+    def free(self, st):
+        st.adam_m = st.adam_v = None
+
+    def step(self, st, s, prof):
+        st.t.step = s
+        if prof is not None:
+            ev0, ev1 = prof.pair()
+            st.t.prof_kernel = self.KERNEL_IDS[prof.kernel]
+            st.t.prof_begin, st.t.prof_end = ev0, ev1
+        _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(st.t), st.stream), "mplc_cnn_train_step")
+
+    def evaluate(self, eng, sel, x, y):
+        """(correct counts, mean CE) of the C models in `sel` [C][STRIDE] on (x, y)."""
+        import torch
+        dev = eng.device
+        stream = _native.stream_handle(dev)
+        n = int(y.numel())
+        C = sel.shape[0]
+        chunk = int(max(32, min(n, eng.eval_budget_bytes // max(1, C * (FEAT + HID) * 4))))
+        chunk = min(chunk, 65535)
+        pooled = torch.empty((C, chunk, FEAT), dtype=torch.float32, device=dev)
+        hidden = torch.empty((C, chunk, HID), dtype=torch.float32, device=dev)
+        correct = torch.zeros(C, dtype=torch.int32, device=dev)
+        loss = torch.zeros(C, dtype=torch.float64, device=dev)
+        _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n, chunk,
+                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(correct),
+                                                 _native.ptr(loss), stream), "mplc_cnn_evaluate")
+        return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
+
+
 class TrainBatch:
-    """Device state of one lockstep batch: coalition global rows, replica rows, Adam state, workspaces."""
+    """Device state of one lockstep batch: coalition global rows, replica rows, optimizer state, workspaces
+    (model-specific parts through eng.model_impl)."""
 
     def __init__(self, eng, coalitions, epochs, lib):
         import torch
         self.eng, self.lib = eng, lib
+        self.model = eng.model_impl
         self.coalitions = coalitions
         self.epochs = epochs
         dev = eng.device
@@ -152,39 +230,20 @@ class TrainBatch:
         self.round_len = round_len
         self.fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
         self.total_steps = max(self.fed_steps, single_steps)
-        splits = (self.bmax + WG_SAMPLES - 1) // WG_SAMPLES
+        S = self.model.STRIDE
         f32 = dict(dtype=torch.float32, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.f32, self.i32 = f32, i32
-        self.glob = torch.empty((C, STRIDE), **f32)
-        self.params = torch.empty((R, STRIDE), **f32)
-        self.adam_m = torch.zeros((R, STRIDE), **f32)
-        self.adam_v = torch.zeros((R, STRIDE), **f32)
+        self.glob = torch.empty((C, S), **f32)
+        self.params = torch.empty((R, S), **f32)
         keys = torch.from_numpy(np.array([init_key(eng.seed, sum(1 << p for p in c)) for c in coalitions],
                                          dtype=np.uint64).view(np.int64)).to(dev)
-        _native.check(lib.mplc_cnn_init_params(_native.ptr(self.glob), STRIDE, _native.ptr(keys), C, self.stream),
-                      "mplc_cnn_init_params")
+        self.model.init_params(self.glob, keys, self.stream)
         src_map = torch.tensor(src, **i32)
-        _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), STRIDE,
+        _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), S,
                                              _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
         self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
-        B = self.bmax
-        self.ws = dict(
-            idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
-            pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
-            hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
-            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, 2, W1P), **f32),
-            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, 9 * 64 * 32), **f32))
-        t = TrainT()
-        t.n_rep, t.bmax, t.w2_splits = R, B, splits
-        t.minibatch_count, t.round_len, t.epochs = M, round_len, epochs
-        t.reps, t.rows, t.splits = self.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
-        t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
-        t.params, t.adam_m, t.adam_v = self.params.data_ptr(), self.adam_m.data_ptr(), self.adam_v.data_ptr()
-        for k, v in self.ws.items():
-            setattr(t, k, v.data_ptr())
-        t.lr, t.beta1, t.beta2, t.eps = 0.001, 0.9, 0.999, 1e-7
-        self.t = t
+        self.model.alloc(self)
         self.stopped = np.zeros(C, dtype=bool)
         self.kind_host = self.rep_arr["kind"].copy()
         self.run_args = self.make_runs()
@@ -218,19 +277,14 @@ class TrainBatch:
         return args
 
     def step(self, s):
-        self.t.step = s
-        prof = self.eng.profiler
-        if prof is not None:
-            ev0, ev1 = prof.pair()
-            self.t.prof_kernel = KERNEL_IDS[prof.kernel]
-            self.t.prof_begin, self.t.prof_end = ev0, ev1
-        _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(self.t), self.stream), "mplc_cnn_train_step")
+        self.model.step(self, s, self.eng.profiler)
 
     def aggregate(self):
+        S, NP = self.model.STRIDE, self.model.NPARAM
         for (r0, c0, nc, first, w, sc) in self.run_args:
-            _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(self.params[r0:]), STRIDE, _native.ptr(first),
-                                                         _native.ptr(w), _native.ptr(sc), nc, NPARAM,
-                                                         _native.ptr(self.glob[c0:c0 + nc]), STRIDE, 1, self.stream),
+            _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(self.params[r0:]), S, _native.ptr(first),
+                                                         _native.ptr(w), _native.ptr(sc), nc, NP,
+                                                         _native.ptr(self.glob[c0:c0 + nc]), S, 1, self.stream),
                           "mplc_fedavg_aggregate")
 
     def stop(self, ci):
@@ -245,14 +299,16 @@ class TrainBatch:
     def finalize(self):
         """Singleton final models -> their coalition rows; free training state."""
         import torch
+        S = self.model.STRIDE
         single = [ci for ci in range(self.C) if self.coal_is_single[ci]]
         if single:
             m = torch.tensor([self.coal_first[ci] for ci in single], **self.i32)
-            tmp = torch.empty((len(single), STRIDE), **self.f32)
-            _native.check(self.lib.mplc_cnn_copy_rows(_native.ptr(tmp), _native.ptr(self.params), STRIDE,
+            tmp = torch.empty((len(single), S), **self.f32)
+            _native.check(self.lib.mplc_cnn_copy_rows(_native.ptr(tmp), _native.ptr(self.params), S,
                                                       _native.ptr(m), len(single), self.stream), "mplc_cnn_copy_rows")
             self.glob[torch.tensor(single, device=self.dev)] = tmp
-        self.params = self.adam_m = self.adam_v = None
+        self.params = None
+        self.model.free(self)
         self.ws = None
         return self.glob
 
@@ -261,7 +317,6 @@ class CnnBatchTrainer:
     """Trains one batch of coalitions (all on the current HIP device) and evaluates them."""
 
     def __init__(self, engine):
-        _bind()
         self.eng = engine
         self.lib = _native.lib()
 
@@ -323,22 +378,8 @@ class CnnBatchTrainer:
     # --------------------------------------------------------------------------------------------
     def _evaluate(self, params, rows, x, y):
         import torch
-        dev = self.eng.device
-        stream = _native.stream_handle(dev)
-        n = int(y.numel())
-        sel = params if rows == list(range(params.shape[0])) else params[torch.tensor(rows, device=dev)].contiguous()
-        C = sel.shape[0]
-        budget = self.eng.eval_budget_bytes
-        chunk = int(max(32, min(n, budget // max(1, C * (FEAT + HID) * 4))))
-        chunk = min(chunk, 65535)
-        pooled = torch.empty((C, chunk, FEAT), dtype=torch.float32, device=dev)
-        hidden = torch.empty((C, chunk, HID), dtype=torch.float32, device=dev)
-        correct = torch.zeros(C, dtype=torch.int32, device=dev)
-        loss = torch.zeros(C, dtype=torch.float64, device=dev)
-        _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n, chunk,
-                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(correct),
-                                                 _native.ptr(loss), stream), "mplc_cnn_evaluate")
-        return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
+        sel = params if rows == list(range(params.shape[0])) else params[torch.tensor(rows, device=self.eng.device)].contiguous()
+        return self.eng.model_impl.evaluate(self.eng, sel, x, y)
 
     def _val_loss(self, params, rows):
         _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)

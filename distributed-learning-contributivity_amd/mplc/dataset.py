@@ -120,6 +120,51 @@ class Mnist(Dataset):
         return train_test_split(x, y, test_size=0.1, random_state=42)
 
 
+def _local_npz(name):
+    dirs = [os.environ.get("MPLC_DATA_DIR", ""), os.path.join(os.getcwd(), "data"),
+            os.path.expanduser("~/.keras/datasets")]
+    for d in dirs:
+        p = os.path.join(d, name) if d else ""
+        if p and os.path.exists(p):
+            with np.load(p, allow_pickle=False) as f:
+                return (f["x_train"], f["y_train"]), (f["x_test"], f["y_test"])
+    return None
+
+
+class Cifar10(Dataset):
+    """mplc/dataset.py:107-210 (model: the engine's batched CIFAR10 CNN, mplc/cifar.py).  Loads a local
+    ``cifar10.npz`` (x_train [50000,32,32,3] uint8, y_train, x_test, y_test) from $MPLC_DATA_DIR, ./data or
+    ~/.keras/datasets - the reference downloads it (mplc/dataset.py:123-150), impossible offline.  Without it,
+    ``synthetic=True`` gives tensors of CIFAR10's exact shapes (x ~ U[0,1) float32, one-hot labels)."""
+
+    def __init__(self, synthetic=None, seed=0, n_train=50000, n_test=10000):
+        loaded = None if synthetic else _local_npz("cifar10.npz")
+        if loaded is None:
+            if synthetic is False:
+                raise FileNotFoundError("cifar10.npz not found (set MPLC_DATA_DIR); no network to download it")
+            rng = np.random.default_rng(seed)
+            x_train = rng.random((n_train, 32, 32, 3), dtype=np.float32)
+            x_test = rng.random((n_test, 32, 32, 3), dtype=np.float32)
+            y_train = _one_hot(rng.integers(0, 10, n_train), 10)
+            y_test = _one_hot(rng.integers(0, 10, n_test), 10)
+            self.synthetic = True
+        else:
+            (xt, yt), (xs, ys) = loaded
+            x_train = xt.astype("float32") / 255  # preprocess_dataset_inputs, mplc/dataset.py:155-160
+            x_test = xs.astype("float32") / 255
+            y_train, y_test = _one_hot(np.asarray(yt).ravel(), 10), _one_hot(np.asarray(ys).ravel(), 10)
+            self.synthetic = False
+        super().__init__("cifar10", (32, 32, 3), 10, x_train, y_train, x_test, y_test)
+
+    @staticmethod
+    def train_test_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+    @staticmethod
+    def train_val_split_local(x, y):
+        return train_test_split(x, y, test_size=0.1, random_state=42)
+
+
 class Titanic(Dataset):
     """mplc/dataset.py:212-394: 27 engineered features, binary label; model = L2 logistic regression
     (the engine's batched exact solver, mplc/lr.py).  Loads a local ``titanic.csv`` (the file the reference
@@ -178,8 +223,10 @@ class ArrayDataset(Dataset):
     """An MNIST-shaped dataset from caller arrays (tests, sklearn digits upsampled, private data).
     Uses the MNIST local splits (train_test_split 0.1, random_state 42, twice)."""
 
-    def __init__(self, x_train, y_train, x_test, y_test, name="mnist", num_classes=10):
-        super().__init__(name, (28, 28, 1), num_classes, x_train, y_train, x_test, y_test)
+    def __init__(self, x_train, y_train, x_test, y_test, name="mnist", num_classes=10, input_shape=None):
+        if input_shape is None:
+            input_shape = tuple(np.asarray(x_train).shape[1:]) if name != "mnist" else (28, 28, 1)
+        super().__init__(name, input_shape, num_classes, x_train, y_train, x_test, y_test)
 
     train_test_split_local = staticmethod(Mnist.train_test_split_local)
     train_val_split_local = staticmethod(Mnist.train_val_split_local)
@@ -202,4 +249,18 @@ def digits_as_mnist(seed=0, noise=0.02):
     return x, y
 
 
-__all__ = ["Dataset", "Mnist", "Titanic", "ArrayDataset", "digits_as_mnist", "constants"]
+def digits_as_cifar(seed=0, noise=0.05):
+    """sklearn's digits upsampled x4 to 32x32 with three differently weighted colour channels and seeded
+    uniform noise: a small, real, learnable CIFAR10-shaped dataset for accuracy tests (no network)."""
+    from sklearn.datasets import load_digits
+    d = load_digits()
+    x = d.images.astype(np.float32) / 16.0
+    x = np.kron(x, np.ones((4, 4), dtype=np.float32))
+    x = np.stack([x, 0.7 * x + 0.3 * x[:, ::-1, :], 0.5 * x + 0.5 * x[:, :, ::-1]], axis=-1)
+    rng = np.random.default_rng(seed)
+    x = (x * (1 - noise) + noise * rng.random(x.shape, dtype=np.float32)).astype(np.float32)
+    return x, _one_hot(d.target, 10)
+
+
+__all__ = ["Dataset", "Mnist", "Cifar10", "Titanic", "ArrayDataset", "digits_as_mnist", "digits_as_cifar",
+           "constants"]

@@ -3,7 +3,8 @@
 Replaces the reference's one-coalition-at-a-time loop (Contributivity.not_twice_characteristic ->
 FederatedAverageLearning/SinglePartnerLearning(...).fit() -> history.score,
 mplc/contributivity.py:92-136, mplc/multi_partner_learning.py:195-334) with batched training of every
-requested coalition in lockstep (mplc/cnn.py, csrc/mnist_cnn.hip).
+requested coalition in lockstep (mplc/cnn.py + csrc/mnist_cnn.hip for MNIST, mplc/cifar.py +
+csrc/cifar_cnn.hip for CIFAR10).
 
 Data live in HBM for the engine's lifetime: the dataset's train/val/test arrays (fp32 images, int32
 labels), and each partner's row indices into the train array (the reference's partner.x_train copies,
@@ -19,7 +20,18 @@ import os
 import numpy as np
 
 from . import constants
-from .cnn import CnnBatchTrainer, minibatch_bounds, STRIDE, FEAT, HID, W1P, W2P
+from .cnn import CnnBatchTrainer, MnistModel, minibatch_bounds
+
+MODELS = {"mnist_cnn": MnistModel}
+
+
+def model_class(name):
+    if name == "cifar10_cnn" and name not in MODELS:
+        from .cifar import CifarModel
+        MODELS[name] = CifarModel
+    if name not in MODELS:
+        raise NotImplementedError(f"model '{name}' has no batched MI355X kernels (see DESIGN.md)")
+    return MODELS[name]
 
 
 class CoalitionEngine:
@@ -31,8 +43,7 @@ class CoalitionEngine:
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("MI355X (HIP) device required: the MPLC engine has no CPU fallback")
-        if model != "mnist_cnn":
-            raise NotImplementedError(f"model '{model}' has no batched MI355X kernels yet (see DESIGN.md)")
+        self.model_impl = model_class(model)()
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.model = model
         self.seed = int(seed)
@@ -42,9 +53,11 @@ class CoalitionEngine:
         self.is_early_stopping = bool(is_early_stopping)
         self.eval_budget_bytes = int(eval_budget_bytes)
 
+        shape = self.model_impl.input_shape
+
         def images(x):
             x = np.asarray(x, dtype=np.float32)
-            return torch.from_numpy(np.ascontiguousarray(x.reshape(x.shape[0], 28, 28))).to(self.device)
+            return torch.from_numpy(np.ascontiguousarray(x.reshape((x.shape[0],) + shape))).to(self.device)
 
         def labels(y):
             y = np.asarray(y)
@@ -87,7 +100,7 @@ class CoalitionEngine:
             target = LogRegEngine
         else:
             target = cls
-        model = {"mnist": "mnist_cnn"}.get(name, name)
+        model = {"mnist": "mnist_cnn", "cifar10": "cifar10_cnn"}.get(name, name)
         parts = scenario.partners_list
         rows = []
         for p in parts:
@@ -107,8 +120,7 @@ class CoalitionEngine:
 
     # --------------------------------------------------------------------------------------------
     def replica_bytes(self, bmax):
-        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + 2 * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
-                + 9 * 64 * 32 * 4 + bmax * 12)
+        return self.model_impl.replica_bytes(bmax)
 
     def plan_batches(self, coalitions):
         """Split coalitions into lockstep batches that fit the HBM budget (cost-sorted so that a batch holds
@@ -118,7 +130,7 @@ class CoalitionEngine:
         for i in order:
             c = coalitions[i]
             bmax = max(self.batch_sizes[p] for p in c)
-            need = len(c) * self.replica_bytes(bmax) + STRIDE * 4
+            need = len(c) * self.replica_bytes(bmax) + self.model_impl.STRIDE * 4
             if cur and (cur_bytes + need > self.memory_budget_bytes or len(cur) >= 65535):
                 batches.append(cur)
                 cur, cur_bytes = [], 0
@@ -132,10 +144,9 @@ class CoalitionEngine:
         """Load the HIP code object (one tiny init_params launch) without running any training kernel."""
         import torch
         from . import _native
-        buf = torch.empty(STRIDE, dtype=torch.float32, device=self.device)
+        buf = torch.empty((1, self.model_impl.STRIDE), dtype=torch.float32, device=self.device)
         keys = torch.zeros(1, dtype=torch.int64, device=self.device)
-        _native.check(_native.lib().mplc_cnn_init_params(_native.ptr(buf), STRIDE, _native.ptr(keys), 1,
-                                                         _native.stream_handle(self.device)), "mplc_cnn_init_params")
+        self.model_impl.init_params(buf, keys, _native.stream_handle(self.device))
         torch.cuda.synchronize(self.device)
 
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):

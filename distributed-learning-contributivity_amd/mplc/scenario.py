@@ -46,6 +46,8 @@ class Scenario:
             self.dataset = dataset
         elif dataset_name == constants.MNIST:
             self.dataset = dataset_module.Mnist()
+        elif dataset_name == constants.CIFAR10:
+            self.dataset = dataset_module.Cifar10()
         elif dataset_name == constants.TITANIC:
             self.dataset = dataset_module.Titanic()
         else:

@@ -115,5 +115,6 @@ int mplc_lr_fedavg(const float* x, const float* y, int n_features, const int32_t
 #endif
 
 #include "mplc_hip_cnn.h"
+#include "mplc_hip_cifar.h"
 
 #endif /* MPLC_HIP_H */
