@@ -23,6 +23,12 @@ SIGNATURES = {
     "mplc_shapley_exact": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mplc_fedavg_aggregate": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p,
                                       c_int64, c_int, c_void_p]),
+    # Monte-Carlo Shapley permutation walks over a dense table (csrc/mc_shapley.hip)
+    "mplc_tmc_walk": (c_int, [c_void_p, c_int, c_void_p, c_int, ctypes.c_double, ctypes.c_double, c_int, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mplc_tmc_moments_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mplc_tmc_moments": (c_int, [c_void_p, c_int, c_void_p, c_uint64, c_uint64, c_int, ctypes.c_double,
+                                 ctypes.c_double, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     # batched CNN trainer (include/mplc_hip_cnn.h); mplc.cnn re-binds train_step with its struct type
     "mplc_cnn_stride": (c_int, []),
     "mplc_cnn_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),

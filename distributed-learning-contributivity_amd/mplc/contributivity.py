@@ -235,15 +235,38 @@ class Contributivity:
     # --------------------------------------------------------------------------------------------
     # Truncated Monte-Carlo (mplc/contributivity.py:195-253) and interpolated TMC (:257-322)
     # --------------------------------------------------------------------------------------------
-    def _prefetch_permutation_wave(self, n, v_all, truncation, wave):
+    def _device_table(self):
+        """The device v(S) table (mplc.mc.VTable) holding every value known to this method so far."""
+        table = getattr(self, "_vtable", None)
+        if table is None:
+            from .mc import VTable
+            table = self._vtable = VTable(self._n)
+        known = dict(self._cache())
+        known.update(self.charac_fct_values)
+        table.update(known)
+        return table
+
+    def _prefetch_permutation_wave(self, n, v_all, truncation, wave, interpolate=False, sizes=None):
         """Draw the next `wave` permutations WITHOUT consuming the global RNG, walk each one's prefixes up
         to its truncation point level by level, and batch-evaluate every uncached prefix of a level at
-        once.  These are exactly the coalitions the sequential loop will ask for on those permutations."""
+        once.  These are exactly the coalitions the sequential loop will ask for on those permutations.
+        With the MI355X engine the walks and their truncation tests run on device (mplc.mc.wave_frontier,
+        csrc/mc_shapley.hip); a plain evaluator (CPU test harness) is walked here in Python."""
         if self._batched_evaluator() is None:
             return
         state = np.random.get_state()
         perms = [np.random.permutation(n) for _ in range(wave)]
         np.random.set_state(state)
+        approach = getattr(self.scenario, "multi_partner_learning_approach", None)
+        if getattr(approach, "device_planning", False) and n <= 24:
+            from .mc import wave_frontier
+
+            def evaluate(keys):
+                self.prefetch(keys)
+                cache = self._cache()
+                return [cache[k] for k in keys]
+            wave_frontier(self._device_table(), np.array(perms), v_all, truncation, interpolate, sizes, evaluate)
+            return
         cache = self._cache()
         known = self.charac_fct_values
 
@@ -286,7 +309,7 @@ class Contributivity:
         while t < 100 or t < q ** 2 * v_max / sv_accuracy ** 2:
             if t >= wave:
                 span = 100 if t < 100 else 50
-                self._prefetch_permutation_wave(n, v_all, truncation, span)
+                self._prefetch_permutation_wave(n, v_all, truncation, span, interpolate, sizes)
                 wave = t + span
             t += 1
             if t > rows.shape[0]:

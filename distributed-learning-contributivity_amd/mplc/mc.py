@@ -1,0 +1,164 @@
+"""Monte-Carlo Shapley on the MI355X: truncated permutation walks over a dense bitmask v(S) table
+(csrc/mc_shapley.hip, include/mplc_hip.h mplc_tmc_*).
+
+Three uses:
+  - VTable: the device copy of the coalition values known so far (NaN = not evaluated), bitmask order.
+  - wave_frontier: walk a wave of permutations on device with the reference's truncation test and return
+    the unknown prefixes they need next (Contributivity's TMCS/ITMCS batch planner).
+  - truncated_mc_table: the reference's truncated_MC / interpol_TMC loop (mplc/contributivity.py:195-322)
+    on a fully known table - rows from the device walk, the sequential stopping rule and moments in numpy
+    exactly as the reference (bit-identical on the reference goldens, tests/test_mc_gpu.py).
+  - tmc_moments: fixed-budget form for large tables (sum / sum of squares per partner reduced on device).
+"""
+import numpy as np
+from scipy.stats import norm
+
+from . import _native
+
+MAX_N = 30
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class VTable:
+    """Dense fp64 v(S) table on device: 2^n entries, NaN = unknown, V[0] = 0."""
+
+    def __init__(self, n, device=None):
+        torch = _torch()
+        if not 1 <= n <= MAX_N:
+            raise ValueError(f"dense table supports 1 <= n <= {MAX_N}")
+        self.n = n
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.V = torch.full((1 << n,), float("nan"), dtype=torch.float64, device=self.device)
+        self.V[0] = 0.0
+        self.known = set()
+
+    @staticmethod
+    def mask(key):
+        m = 0
+        for i in key:
+            m |= 1 << int(i)
+        return m
+
+    def update(self, values):
+        """values: {sorted tuple of partner ids: v}; uploads the entries not on the device yet."""
+        torch = _torch()
+        new = [(self.mask(k), float(v)) for k, v in values.items() if len(k) and k not in self.known]
+        if not new:
+            return
+        idx = torch.tensor([m for m, _ in new], dtype=torch.int64, device=self.device)
+        val = torch.tensor([v for _, v in new], dtype=torch.float64, device=self.device)
+        self.V.index_put_((idx,), val)
+        self.known.update(k for k, v in values.items() if len(k))
+
+    @classmethod
+    def from_array(cls, V, device=None):
+        torch = _torch()
+        V = np.asarray(V, dtype=np.float64)
+        n = int(V.size).bit_length() - 1
+        if V.size != 1 << n:
+            raise ValueError("table length must be a power of two")
+        t = cls.__new__(cls)
+        t.n = n
+        t.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        t.V = torch.from_numpy(V.copy()).to(t.device)
+        t.known = None
+        return t
+
+
+def tmc_walk(table, perms, v_all, truncation, interpolate=False, sizes=None):
+    """Device walk of each permutation (rows [K][n] fp64, status [K] int32, need [K] uint64 masks)."""
+    torch = _torch()
+    perms = np.ascontiguousarray(perms, dtype=np.uint8)
+    K, n = perms.shape
+    if n != table.n:
+        raise ValueError("permutation length does not match the table")
+    dev = table.device
+    p_d = torch.from_numpy(perms).to(dev)
+    rows = torch.empty((K, n), dtype=torch.float64, device=dev)
+    status = torch.empty(K, dtype=torch.int32, device=dev)
+    need = torch.empty(K, dtype=torch.int64, device=dev)
+    sz = torch.tensor(np.asarray(sizes, dtype=np.float64), device=dev) if sizes is not None else None
+    _native.check(_native.lib().mplc_tmc_walk(_native.ptr(table.V), n, _native.ptr(p_d), K, float(v_all),
+                                              float(truncation), int(bool(interpolate)), _native.ptr(sz),
+                                              _native.ptr(rows), _native.ptr(status), _native.ptr(need),
+                                              _native.stream_handle(dev)), "mplc_tmc_walk")
+    return rows.cpu().numpy(), status.cpu().numpy(), need.cpu().numpy().view(np.uint64)
+
+
+def mask_to_key(mask):
+    mask = int(mask)
+    return tuple(i for i in range(mask.bit_length()) if (mask >> i) & 1)
+
+
+def wave_frontier(table, perms, v_all, truncation, interpolate, sizes, evaluate):
+    """Walk `perms` on device; while walks stop on unknown prefixes, evaluate those prefixes in one batch
+    (`evaluate(list of keys) -> values`), publish them to the table and walk again.  Returns the rows."""
+    while True:
+        rows, status, need = tmc_walk(table, perms, v_all, truncation, interpolate, sizes)
+        missing = sorted({int(m) for m, s in zip(need, status) if s < table.n})
+        if not missing:
+            return rows
+        keys = [mask_to_key(m) for m in missing]
+        vals = evaluate(keys)
+        table.update(dict(zip(keys, (float(v) for v in vals))))
+
+
+def truncated_mc_table(table, sv_accuracy=0.01, alpha=0.95, truncation=0.05, interpolate=False, sizes=None,
+                       wave=100):
+    """The reference TMCS / ITMCS loop (mplc/contributivity.py:215-246 / :276-316) on a fully known table:
+    permutations from numpy's global RNG in the reference's order, rows computed on device in waves drawn
+    ahead from a saved RNG state, stopping rule and moments in numpy.  Returns (sv, std, t)."""
+    n = table.n
+    v_all = float(table.V[(1 << n) - 1].item())
+    q = norm.ppf((1 - alpha) / 2, loc=0, scale=1)
+    contributions = np.zeros((0, n))
+    t, v_max = 0, 0
+    buf, pos = None, 0
+    while t < 100 or t < q ** 2 * v_max / sv_accuracy ** 2:
+        if buf is None or pos == len(buf[0]):
+            state = np.random.get_state()
+            perms = np.array([np.random.permutation(n) for _ in range(wave)])
+            np.random.set_state(state)
+            rows, status, _ = tmc_walk(table, perms, v_all, truncation, interpolate, sizes)
+            if np.any(status < n):
+                raise ValueError("truncated_mc_table needs a fully known table")
+            buf, pos = (perms, rows), 0
+        t += 1
+        perm = np.random.permutation(n)
+        assert np.array_equal(perm, buf[0][pos])
+        contributions = np.vstack((contributions, buf[1][pos][None, :])) if t > 1 else buf[1][pos][None, :].copy()
+        pos += 1
+        v_max = np.max(np.var(contributions, axis=0))
+    return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1), t
+
+
+def tmc_moments(table, n_perms, v_all=None, truncation=0.05, interpolate=False, sizes=None, perms=None, seed=0,
+                perm_base=0):
+    """Fixed-budget TMCS on device: (mean, std, complete) over n_perms walks (perms given or keyed on device)."""
+    torch = _torch()
+    n = table.n
+    dev = table.device
+    if v_all is None:
+        v_all = float(table.V[(1 << n) - 1].item())
+    lib = _native.lib()
+    ws_bytes = int(lib.mplc_tmc_moments_workspace_bytes(n, int(n_perms)))
+    ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev)
+    out = torch.empty(2 * n + 1, dtype=torch.float64, device=dev)
+    p_d = torch.from_numpy(np.ascontiguousarray(perms, dtype=np.uint8)).to(dev) if perms is not None else None
+    sz = torch.tensor(np.asarray(sizes, dtype=np.float64), device=dev) if sizes is not None else None
+    _native.check(lib.mplc_tmc_moments(_native.ptr(table.V), n, _native.ptr(p_d), int(seed), int(perm_base),
+                                       int(n_perms), float(v_all), float(truncation), int(bool(interpolate)),
+                                       _native.ptr(sz), _native.ptr(out), _native.ptr(ws), ws_bytes,
+                                       _native.stream_handle(dev)), "mplc_tmc_moments")
+    m = out.cpu().numpy()
+    k = m[2 * n]
+    mean = m[:n] / k
+    var = np.maximum(m[n:2 * n] / k - mean ** 2, 0.0)
+    return mean, np.sqrt(var), int(k)
+
+
+__all__ = ["VTable", "tmc_walk", "wave_frontier", "truncated_mc_table", "tmc_moments", "mask_to_key"]

@@ -75,6 +75,9 @@ class MultiPartnerLearning:
         self.history.nb_epochs_done = int(res["epochs_done"][0])
         self.learning_computation_time = timer() - start
 
+    # Contributivity plans TMCS/ITMCS permutation waves with the device walk (mplc.mc) for this approach
+    device_planning = True
+
     @classmethod
     def evaluate_coalitions(cls, scenario, coalitions):
         """Batched v(S) for many coalitions (test accuracy of the trained coalition model), float64 array.

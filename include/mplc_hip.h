@@ -102,6 +102,28 @@ int mplc_lr_fedavg(const float* x, const float* y, int n_features, const int32_t
                    void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Monte-Carlo Shapley over a dense bitmask v(S) table (csrc/mc_shapley.hip).  V has 2^n fp64 entries,
+ * NaN = not evaluated yet; 1 <= n <= 30; perms are [n_perms][n] uint8 partner ids.
+ * Replaces: the permutation walk of truncated_MC / interpol_TMC (mplc/contributivity.py:217-246,
+ *           :278-316): char[j+1] = char[j] (TMCS) / char[j] + a*size[j] (ITMCS, sizes in partner-index
+ *           order as the reference) once |v_all - char[j]| < truncation, else v(prefix); row[perm[j]] =
+ *           char[j+1] - char[j], in the reference's fp64 operation order.
+ * ---------------------------------------------------------------------------------------------- */
+
+/* One thread per permutation: rows[k][n] increments; status[k] = n if the walk completed, else the first
+ * position j whose prefix mask need[k] is NaN in V (rows[k] then incomplete). */
+int mplc_tmc_walk(const double* V, int n, const uint8_t* perms, int n_perms, double v_all, double truncation,
+                  int interpolate, const double* sizes, double* rows, int32_t* status, uint64_t* need, void* stream);
+
+/* Fixed-budget form: moments_out[2n+1] = {sum_k row_k[j] (j<n), sum_k row_k[j]^2 (j<n), #complete walks}
+ * over n_perms walks (incomplete walks contribute 0).  perms == NULL draws permutation perm_base + k on
+ * device (keyed Fisher-Yates from `seed`).  Deterministic reduction (wavefront shuffles, fixed block order). */
+size_t mplc_tmc_moments_workspace_bytes(int n, int n_perms);
+int mplc_tmc_moments(const double* V, int n, const uint8_t* perms, uint64_t seed, uint64_t perm_base, int n_perms,
+                     double v_all, double truncation, int interpolate, const double* sizes, double* moments_out,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Batched multi-model MNIST CNN trainer (mplc/dataset.py:457-479 architecture; Keras 2.3.1 Adam).
  * One "replica" = one (coalition, partner) model.  Replaces, for B replicas at once, the per-partner
  * Keras `model.fit(x_mb, y_mb, batch_size=bs_p, epochs=1)` of mplc/multi_partner_learning.py:319-332

@@ -34,7 +34,7 @@ def parse_table(case):
     return table
 
 
-def make_scenario(case, calls, batched=False):
+def make_scenario(case, calls, batched=False, device_planning=False):
     table = parse_table(case)
 
     class FakeMPL:
@@ -54,14 +54,15 @@ def make_scenario(case, calls, batched=False):
                 calls.append(tuple(c))
             return np.array([table[tuple(c)] for c in coalitions])
         FakeMPL.evaluate_coalitions = staticmethod(evaluate_coalitions)
+        FakeMPL.device_planning = device_planning
 
     partners = [types.SimpleNamespace(id=i, y_train=np.zeros(s)) for i, s in enumerate(case["sizes"])]
     return types.SimpleNamespace(partners_list=partners, multi_partner_learning_approach=FakeMPL), FakeMPL
 
 
-def run_case(case, monkeypatch, batched=False):
+def run_case(case, monkeypatch, batched=False, device_planning=False):
     calls = []
-    scenario, fake = make_scenario(case, calls, batched)
+    scenario, fake = make_scenario(case, calls, batched, device_planning)
     monkeypatch.setattr(mpl_mod, "SinglePartnerLearning", fake)
     np.random.seed(case["seed"])
     c = Contributivity(scenario=scenario)
