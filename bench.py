@@ -13,6 +13,11 @@ leg "train" (default; BASELINE.json metric "coalition v(S) evals/sec (MNIST FedA
   the job is fixed).
   Also reported: "shapley_agg" - the exact-Shapley aggregation kernel on a 2^28 fp64 table (config #5).
 leg "shapley": only the N=28 aggregation (GB/s).
+leg "cifar" (BASELINE config #4): CIFAR10 CNN, 20 partners, FedAvg, "TMCS" (default; --method SMCS etc.) with
+  the reference's defaults (sv_accuracy .01, alpha .95, truncation .05), fixed E=1, M=20, G=8.  CIFAR10-shaped
+  synthetic data with class templates (signal 0.4: accuracy grows with the data a coalition holds, so the
+  truncation behaves as on real data; CIFAR10 itself cannot be fetched).  One step = one full
+  compute_contributivity(method) with numpy seeded 0; value = distinct coalitions evaluated / second.
 """
 import argparse
 import json
@@ -285,12 +290,120 @@ def bench_train(args, rank, world):
     return out, sc
 
 
+# --------------------------------------------------------------------------------------------------
+# CIFAR10 TMCS/SMCS leg (config #4)
+# --------------------------------------------------------------------------------------------------
+def build_cifar_scenario(epochs, signal):
+    import numpy as np
+    from mplc.dataset import Cifar10
+    from mplc.scenario import Scenario
+    amounts = [0.05] * 19 + [float(1 - np.sum([0.05] * 19))]  # [0.05]*20 fails the reference's sum check
+    sc = Scenario(20, amounts, dataset=Cifar10(synthetic=True, signal=signal), minibatch_count=20,
+                  gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False)
+    return sc.provision()
+
+
+def cpu_baseline_cifar(sc, coalitions, epochs, M, budget_s=25.0):
+    """Oracle (torch-CPU fp32, sequential like the reference) on a bounded sample: one singleton and one
+    pair; FedAvg cost is linear in |S|, so the evaluated coalition list is extrapolated from t(1), t(2)."""
+    import torch
+    from oracle import cifar_cnn as occ
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ds = sc.dataset
+    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    times = {}
+    for k in (1, 2):
+        t0 = time.perf_counter()
+        occ.coalition_value(data, prow, bs, tuple(range(k)), epochs=epochs, M=M)
+        times[k] = time.perf_counter() - t0
+    per_partner = times[2] / 2.0
+    total = sum(times[1] if len(c) == 1 else per_partner * len(c) for c in coalitions)
+    return {"value": round(len(coalitions) / total, 5), "unit": "coalition evals/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle torch-CPU fp32 sequential fits (E={epochs}, M={M}) of |S|=1: {times[1]:.1f}s and |S|=2: "
+                       f"{times[2]:.1f}s; the {len(coalitions)} coalitions this TMCS run evaluated extrapolated "
+                       f"linearly in |S|: {total:.0f}s")}
+
+
+def bench_cifar(args, rank, world):
+    import numpy as np
+    from mplc.cifar import FLOP_PER_SAMPLE
+    from mplc.contributivity import Contributivity
+    from mplc.engine import CoalitionEngine
+    from mplc.profiling import KernelTimer
+    sc = build_cifar_scenario(args.cifar_epochs, args.signal)
+    sc.engine = CoalitionEngine.for_scenario(sc)
+    eng = sc.engine
+    eng.warmup()
+    t_start = time.perf_counter()
+
+    def progress(s, total, R):  # the run is long: keep a heartbeat on stderr
+        if s == 0:
+            print(f"[bench cifar {time.perf_counter() - t_start:7.1f}s] batch of {R} replicas, {total} steps, "
+                  f"{eng.stats['coalitions']} coalitions so far", file=sys.stderr, flush=True)
+    eng.progress = progress
+
+    def one_step():
+        sc.coalition_values = {}
+        np.random.seed(0)
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity(args.method)
+        return c
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier(world)
+    timer = KernelTimer(args.cifar_profile_kernel)
+    eng.profiler = timer
+    s0 = eng.stats["samples"]
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        c = one_step()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    eng.profiler = None
+    kern_ms = timer.total_ms()
+    launches = timer.launches()
+    samples = eng.stats["samples"] - s0
+    flops = samples * FLOP_PER_SAMPLE[args.cifar_profile_kernel]
+    achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
+    evals = c.first_charac_fct_calls_count
+    coals = [k for k in c.charac_fct_values if len(k)]
+    out = {
+        "metric": f"coalition v(S) evals/sec (CIFAR10 FedAvg, {args.method})",
+        "value": round(evals * args.steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1000 / args.steps, 1),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (CIFAR10-shaped: x = 0.4 class template + 0.6 U[0,1) fp32 [50000,32,32,3], one-hot labels)",
+        "config": {"workload": f"BASELINE config #4: CIFAR10 CNN, 20 partners, FedAvg, {args.method} (reference defaults, "
+                               f"numpy seed 0), E={args.cifar_epochs} fixed, M=20, G=8, coalitions LPT-sharded x{world}",
+                   "partners": 20, "method": args.method, "coalitions_evaluated": evals,
+                   "coalition_sizes": {str(k): sum(1 for c_ in coals if len(c_) == k) for k in range(1, 21)},
+                   "train_samples_per_step_this_rank": int(samples / max(1, args.steps)),
+                   "shapley_estimate": [round(float(v), 5) for v in c.contributivity_scores],
+                   "parallelism": f"coalition-shard x{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": args.cifar_profile_kernel, "launches": launches,
+                     "kernel_ms_avg": round(kern_ms / max(1, launches), 4),
+                     "algorithmic_flop_per_launch": int(flops / max(1, launches)),
+                     "flop_per_sample": FLOP_PER_SAMPLE[args.cifar_profile_kernel]},
+    }
+    return out, sc, coals
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=0)
-    ap.add_argument("--leg", default="train", choices=["train", "shapley"])
+    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar"])
+    ap.add_argument("--method", default="TMCS")
+    ap.add_argument("--signal", type=float, default=0.4)
+    ap.add_argument("--cifar-epochs", type=int, default=1)
+    ap.add_argument("--cifar-profile-kernel", default="conv2_fwd")
     ap.add_argument("--partners", type=int, default=10)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--minibatches", type=int, default=20)
@@ -309,6 +422,11 @@ def main():
                                                                 f"range-sharded + RCCL all-reduce x{world}"}})
         if rank == 0:
             out["cpu_baseline"] = cpu_baseline_shapley() if (world == 1 and not args.no_cpu_baseline) else None
+    elif args.leg == "cifar":
+        out, sc, coals = bench_cifar(args, rank, world)
+        if rank == 0:
+            out["cpu_baseline"] = (cpu_baseline_cifar(sc, coals, args.cifar_epochs, 20)
+                                   if (world == 1 and not args.no_cpu_baseline) else None)
     else:
         out, sc = bench_train(args, rank, world)
         wl = out["config"]["workload"]

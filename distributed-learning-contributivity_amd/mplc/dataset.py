@@ -88,6 +88,24 @@ def _one_hot(y, k):
     return np.eye(k, dtype="float32")[np.asarray(y, dtype=np.int64).ravel()]
 
 
+def _synthetic_images(shape, n_train, n_test, seed, signal=0.0):
+    """Dataset-shaped synthetic images, x in [0,1) float32, one-hot labels of 10 classes.  signal = 0: pure
+    uniform noise with random labels (throughput work, every model at chance).  signal > 0: x = signal *
+    template[y] + (1 - signal) * noise with one fixed random template per class, so accuracy grows with the
+    amount of training data - truncated Monte-Carlo estimators then behave as on real data."""
+    rng = np.random.default_rng(seed)
+    y_train = rng.integers(0, 10, n_train)
+    y_test = rng.integers(0, 10, n_test)
+    x_train = rng.random((n_train,) + shape, dtype=np.float32)
+    x_test = rng.random((n_test,) + shape, dtype=np.float32)
+    if signal > 0:
+        tmpl = np.random.default_rng(seed + 1).random((10,) + shape, dtype=np.float32)
+        s = np.float32(signal)
+        x_train = (s * tmpl[y_train] + (np.float32(1) - s) * x_train).astype(np.float32)
+        x_test = (s * tmpl[y_test] + (np.float32(1) - s) * x_test).astype(np.float32)
+    return x_train, _one_hot(y_train, 10), x_test, _one_hot(y_test, 10)
+
+
 class Mnist(Dataset):
     """mplc/dataset.py:397-488 (model: the engine's batched CNN of the same architecture)."""
 
@@ -137,16 +155,12 @@ class Cifar10(Dataset):
     ~/.keras/datasets - the reference downloads it (mplc/dataset.py:123-150), impossible offline.  Without it,
     ``synthetic=True`` gives tensors of CIFAR10's exact shapes (x ~ U[0,1) float32, one-hot labels)."""
 
-    def __init__(self, synthetic=None, seed=0, n_train=50000, n_test=10000):
+    def __init__(self, synthetic=None, seed=0, n_train=50000, n_test=10000, signal=0.0):
         loaded = None if synthetic else _local_npz("cifar10.npz")
         if loaded is None:
             if synthetic is False:
                 raise FileNotFoundError("cifar10.npz not found (set MPLC_DATA_DIR); no network to download it")
-            rng = np.random.default_rng(seed)
-            x_train = rng.random((n_train, 32, 32, 3), dtype=np.float32)
-            x_test = rng.random((n_test, 32, 32, 3), dtype=np.float32)
-            y_train = _one_hot(rng.integers(0, 10, n_train), 10)
-            y_test = _one_hot(rng.integers(0, 10, n_test), 10)
+            x_train, y_train, x_test, y_test = _synthetic_images((32, 32, 3), n_train, n_test, seed, signal)
             self.synthetic = True
         else:
             (xt, yt), (xs, ys) = loaded

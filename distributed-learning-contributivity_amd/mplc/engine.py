@@ -86,7 +86,7 @@ class CoalitionEngine:
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): HIP events around one kernel per step
-        self.stats = {"coalitions": 0, "batches": 0, "replicas": 0}
+        self.stats = {"coalitions": 0, "batches": 0, "replicas": 0, "samples": 0}
 
     # --------------------------------------------------------------------------------------------
     @classmethod
@@ -166,6 +166,9 @@ class CoalitionEngine:
             epochs_done[batch] = e
             self.stats["batches"] += 1
             self.stats["replicas"] += sum(len(c) for c in coal)
+            # samples trained (every replica sees all its partner's rows once per epoch done)
+            self.stats["samples"] += int(sum(int(ep) * sum(self.partner_sizes[p] for p in c)
+                                             for c, ep in zip(coal, e)))
         self.stats["coalitions"] += len(coalitions)
         if return_details:
             return {"scores": scores, "epochs_done": epochs_done}
