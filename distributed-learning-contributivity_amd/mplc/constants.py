@@ -33,3 +33,5 @@ TITANIC = "titanic"
 SUPPORTED_DATASETS_NAMES = [MNIST, CIFAR10, TITANIC]
 
 EXPERIMENTS_FOLDER_NAME = "experiments"
+INFO_LOGGING_FILE_NAME = "info.log"
+DEBUG_LOGGING_FILE_NAME = "debug.log"

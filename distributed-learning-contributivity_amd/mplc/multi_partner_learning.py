@@ -68,6 +68,17 @@ class MultiPartnerLearning:
 
     def fit(self):
         start = timer()
+        key = self._coalition()
+        cache = getattr(self.scenario, "coalition_values", None)
+        # the cache holds v(S) as Contributivity defines it: the scenario's epochs, early stopping ON
+        # (mplc/contributivity.py:100-112); reuse it only for a fit with the same semantics
+        same = (self.epoch_count == getattr(self.scenario, "epoch_count", self.epoch_count)
+                and (self.is_early_stopping or self.epoch_count <= constants.PATIENCE))
+        if same and cache is not None and key in cache:  # evaluated earlier (or loaded from a persisted table)
+            self.history.score = float(cache[key])
+            self.history.nb_epochs_done = int(getattr(self.scenario, "coalition_epochs", {}).get(key, self.epoch_count))
+            self.learning_computation_time = timer() - start
+            return
         eng = _engine(self.scenario)
         res = eng.evaluate([self._coalition()], epoch_count=self.epoch_count,
                            is_early_stopping=self.is_early_stopping, return_details=True)
@@ -84,7 +95,10 @@ class MultiPartnerLearning:
         Under torch.distributed the coalitions are LPT-sharded over the ranks (mplc.parallel)."""
         from .parallel import sharded_evaluate
         eng = _engine(scenario)
-        return sharded_evaluate(eng.evaluate, list(coalitions), eng.partner_sizes, eng.device)
+
+        def local(cs):  # Contributivity always builds its learners with is_early_stopping=True
+            return eng.evaluate(cs, is_early_stopping=True)
+        return sharded_evaluate(local, list(coalitions), eng.partner_sizes, eng.device)
 
 
 class SinglePartnerLearning(MultiPartnerLearning):

@@ -27,7 +27,7 @@ logger = logging.getLogger("mplc")
 PARAMS_KNOWN = ["dataset", "dataset_name", "dataset_proportion", "methods", "multi_partner_learning_approach",
                 "aggregation", "partners_count", "amounts_per_partner", "corrupted_datasets", "samples_split_option",
                 "gradient_updates_per_pass_count", "epoch_count", "minibatch_count", "is_early_stopping",
-                "init_model_from", "is_quick_demo", "engine_seed"]
+                "init_model_from", "is_quick_demo", "engine_seed", "coalition_values_file"]
 
 
 class Scenario:
@@ -38,7 +38,8 @@ class Scenario:
                  gradient_updates_per_pass_count=constants.DEFAULT_GRADIENT_UPDATES_PER_PASS_COUNT,
                  minibatch_count=constants.DEFAULT_BATCH_COUNT, epoch_count=constants.DEFAULT_EPOCH_COUNT,
                  is_early_stopping=True, methods=None, is_quick_demo=False, experiment_path=Path("./experiments"),
-                 scenario_id=1, repeats_count=1, is_dry_run=True, engine_seed=0, **kwargs):
+                 scenario_id=1, repeats_count=1, is_dry_run=True, engine_seed=0, coalition_values_file=None,
+                 **kwargs):
         unknown = [k for k in kwargs if k not in PARAMS_KNOWN]
         if unknown:
             raise Exception(f"Unrecognised parameters {unknown}, check your configuration")
@@ -108,6 +109,8 @@ class Scenario:
             self.save_folder.mkdir(parents=True, exist_ok=True)
         self.engine = None
         self.coalition_values = {}
+        # opt-in persisted v(S) table shared across methods and runs (npz, bitmask order)
+        self.coalition_values_file = coalition_values_file
 
     # --------------------------------------------------------------------------------------------
     def instantiate_scenario_partners(self):
@@ -179,15 +182,70 @@ class Scenario:
         """mplc/scenario.py:845-879: grand-coalition learning, then each contributivity method."""
         from .contributivity import Contributivity
         self.provision()
+        if self.coalition_values_file:
+            self.load_coalition_values(self.coalition_values_file, missing_ok=True)
         self.mpl = self.multi_partner_learning_approach(self, is_save_data=True)
         self.mpl.fit()
-        self.coalition_values[tuple(range(self.partners_count))] = self.mpl.history.score
+        if self.is_early_stopping or self.epoch_count <= constants.PATIENCE:  # same v(N) as Contributivity's
+            self.coalition_values[tuple(range(self.partners_count))] = self.mpl.history.score
         for method in self.methods:
             contrib = Contributivity(scenario=self)
             contrib.compute_contributivity(method)
             self.contributivity_list.append(contrib)
             logger.info(f"## Evaluating contributivity with {method}: {contrib}")
+        if self.coalition_values_file:
+            self.save_coalition_values(self.coalition_values_file)
         return 0
+
+    # --------------------------------------------------------------------------------------------
+    # persisted v(S) table
+    # --------------------------------------------------------------------------------------------
+    def coalition_values_fingerprint(self):
+        """Everything a v(S) depends on; a table saved under another fingerprint is never reused."""
+        import json
+        import zlib
+        approach = self.multi_partner_learning_approach
+        ds = self.dataset
+        content = zlib.crc32(np.ascontiguousarray(ds.y_train).tobytes())
+        content = zlib.crc32(np.ascontiguousarray(np.asarray(ds.x_train)[::97]).tobytes(), content)
+        content = zlib.crc32(np.ascontiguousarray(np.asarray(ds.x_test)[::97]).tobytes(), content)
+        return json.dumps({
+            "content_crc32": int(content),
+            "dataset": self.dataset.name, "synthetic": bool(getattr(self.dataset, "synthetic", False)),
+            "n_train": int(len(self.dataset.x_train)), "n_val": int(len(self.dataset.x_val)),
+            "n_test": int(len(self.dataset.x_test)),
+            "partners": [int(len(p.train_idx)) for p in self.partners_list],
+            "batch_sizes": [int(p.batch_size) for p in self.partners_list],
+            "split": [self.samples_split_type, str(self.samples_split_description)],
+            "approach": getattr(approach, "__name__", str(approach)), "aggregation": self.aggregation,
+            "epoch_count": self.epoch_count, "minibatch_count": self.minibatch_count,
+            "gradient_updates_per_pass_count": self.gradient_updates_per_pass_count,
+            "is_early_stopping": bool(self.is_early_stopping), "engine_seed": self.engine_seed,
+            "dataset_proportion": self.dataset_proportion}, sort_keys=True)
+
+    def save_coalition_values(self, path):
+        """Write the known v(S) as npz: masks (uint64, bit i = partner i), values (float64), fingerprint."""
+        keys = sorted(k for k in self.coalition_values if len(k))
+        masks = np.array([sum(1 << int(i) for i in k) for k in keys], dtype=np.uint64)
+        values = np.array([float(self.coalition_values[k]) for k in keys], dtype=np.float64)
+        np.savez(path, masks=masks, values=values, n=np.int64(self.partners_count),
+                 fingerprint=np.array(self.coalition_values_fingerprint()))
+
+    def load_coalition_values(self, path, missing_ok=False):
+        """Merge a saved table into the coalition cache (the memo and call counts of each method are
+        unaffected: only the training is skipped).  Returns the number of entries loaded."""
+        import os
+        if not os.path.exists(path):
+            if missing_ok:
+                return 0
+            raise FileNotFoundError(path)
+        with np.load(path, allow_pickle=False) as f:
+            if str(f["fingerprint"]) != self.coalition_values_fingerprint() or int(f["n"]) != self.partners_count:
+                raise ValueError(f"{path} was computed for another scenario configuration")
+            for m, v in zip(f["masks"], f["values"]):
+                m = int(m)
+                self.coalition_values[tuple(i for i in range(self.partners_count) if (m >> i) & 1)] = float(v)
+            return int(len(f["values"]))
 
     def append_contributivity(self, contributivity):
         self.contributivity_list.append(contributivity)
