@@ -125,7 +125,8 @@ __global__ void init_params_kernel(float* __restrict__ params, int64_t stride, c
 }
 
 __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_rep, int bmax,
-                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits, int step,
+                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits,
+                                const int32_t* __restrict__ seq, int step,
                                 int M, int round_len, int epochs, int32_t* __restrict__ idx,
                                 int32_t* __restrict__ cnt, int32_t* __restrict__ opt_t,
                                 uint64_t* __restrict__ drop_key) {
@@ -133,7 +134,7 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
   if (gid >= (int64_t)n_rep * bmax) return;
   const int r = (int)(gid / bmax);
   const int j = (int)(gid % bmax);
-  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits);
+  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits, seq);
   idx[gid] = ss.row;
   if (j == 0) {
     cnt[r] = ss.c;
@@ -970,7 +971,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int R = t->n_rep, B = t->bmax;
   const int64_t slots = (int64_t)R * B;
-  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->step,
+  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->opt_t, t->drop_key);
   enqueue_forward(s, R, B, t->x, 1, 0, t->idx, t->cnt, 0, t->params, STRIDE, t->drop_key, t->a1, t->d2, t->code2,

@@ -51,11 +51,70 @@ struct SlotSched {
   uint64_t dkey;
 };
 
+// Sequential coalition model at one step: which member trains (index mi in ascending partner order), the
+// Keras step tl inside that member's fit, its step count ns, and the member record.  Round (e, m) visits
+// the members in the keyed order keyed_perm(subkey(key, 0x60000 + e, m), k, .) (the reference draws
+// np.random.permutation(partners_count), mplc/multi_partner_learning.py:365); each member fit runs
+// ceil(L / bs) steps on its minibatch m, back to back from the start of the round.
+struct SeqPos {
+  int e, m, t, mi, tl, ns;
+  const int32_t* rec;
+};
+
+__device__ __forceinline__ bool seq_locate(const mplc_replica_t& rep, int step, int M, int round_len, int epochs,
+                                           const int32_t* __restrict__ splits, const int32_t* __restrict__ seq,
+                                           SeqPos& p) {
+  const int per_epoch = M * round_len;
+  p.e = step / per_epoch;
+  if (p.e >= epochs) return false;
+  const int rem = step % per_epoch;
+  p.m = rem / round_len;
+  p.t = rem % round_len;
+  const int k = rep.n_rows;
+  const uint64_t okey = subkey(rep.key, 0x60000u + (uint32_t)p.e, (uint32_t)p.m);
+  int acc = 0;
+  for (int idx = 0; idx < k; ++idx) {
+    const int mi = (int)keyed_perm(okey, (uint32_t)k, (uint32_t)idx);
+    const int32_t* rec = seq + rep.rows_off + MPLC_SEQ_REC * mi;
+    const int L = splits[rec[3] + p.m + 1] - splits[rec[3] + p.m];
+    const int ns = (L + rec[1] - 1) / rec[1];
+    if (p.t < acc + ns) {
+      p.mi = mi;
+      p.tl = p.t - acc;
+      p.ns = ns;
+      p.rec = rec;
+      return true;
+    }
+    acc += ns;
+  }
+  return false;  // this coalition's round is shorter than round_len: idle
+}
+
 __device__ __forceinline__ SlotSched schedule_slot(const mplc_replica_t& rep, int j, int step, int M, int round_len,
                                                    int epochs, const int32_t* __restrict__ rows,
-                                                   const int32_t* __restrict__ splits) {
+                                                   const int32_t* __restrict__ splits,
+                                                   const int32_t* __restrict__ seq) {
   SlotSched s{0, 0, -1, 0ull};
-  if (rep.kind == MPLC_REP_FEDAVG) {
+  if (rep.kind == MPLC_REP_SEQ) {
+    SeqPos p;
+    if (seq_locate(rep, step, M, round_len, epochs, splits, seq, p)) {
+      const int32_t* rec = p.rec;
+      const int n_rows = rec[0], batch = rec[1], rows_off = rec[2], split_off = rec[3];
+      const uint64_t mkey = (uint64_t)(uint32_t)rec[4] | ((uint64_t)(uint32_t)rec[5] << 32);
+      const int s0 = splits[split_off + p.m];
+      const int L = splits[split_off + p.m + 1] - s0;
+      s.c = min(batch, L - p.tl * batch);
+      s.at = p.t + 1;  // one optimizer for the whole round: its iterations run on across the members
+      s.dkey = subkey(mkey, 0x40000u + (uint32_t)p.e, ((uint32_t)p.m << 16) | (uint32_t)p.tl);
+      if (j < s.c) {
+        const uint32_t q = keyed_perm(subkey(mkey, 0x20000u + (uint32_t)p.e, (uint32_t)p.m), (uint32_t)L,
+                                      (uint32_t)(p.tl * batch + j));
+        const uint32_t pos = keyed_perm(subkey(mkey, 0x10000u + (uint32_t)p.e, 0u), (uint32_t)n_rows,
+                                        (uint32_t)s0 + q);
+        s.row = rows[rows_off + (int)pos];
+      }
+    }
+  } else if (rep.kind == MPLC_REP_FEDAVG) {
     const int per_epoch = M * round_len;
     const int e = step / per_epoch;
     const int rem = step % per_epoch;

@@ -120,14 +120,15 @@ __global__ void copy_rows_kernel(float* __restrict__ dst, const float* __restric
 // Schedule: global step -> per-replica sample rows (reference sample order, keyed permutations)
 // ------------------------------------------------------------------------------------------------
 __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_rep, int bmax,
-                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits, int step,
+                                const int32_t* __restrict__ rows, const int32_t* __restrict__ splits,
+                                const int32_t* __restrict__ seq, int step,
                                 int M, int round_len, int epochs, int32_t* __restrict__ idx,
                                 int32_t* __restrict__ cnt, int32_t* __restrict__ adam_t) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)n_rep * bmax) return;
   const int r = (int)(gid / bmax);
   const int j = (int)(gid % bmax);
-  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits);
+  const SlotSched ss = schedule_slot(reps[r], j, step, M, round_len, epochs, rows, splits, seq);
   const int c = ss.c, at = ss.at, row = ss.row;
   idx[gid] = row;
   if (j == 0) {
@@ -908,7 +909,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   const int R = t->n_rep, B = t->bmax;
   const int64_t S = MPLC_CNN_STRIDE;
   const int64_t slots = (int64_t)R * B;
-  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->step,
+  schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t);
   PROF_BEGIN(1);

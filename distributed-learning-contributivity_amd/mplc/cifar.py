@@ -36,7 +36,7 @@ class CifarTrainT(ctypes.Structure):
     _fields_ = ([("n_rep", ctypes.c_int32), ("bmax", ctypes.c_int32), ("wg_splits", ctypes.c_int32),
                  ("pad0", ctypes.c_int32), ("step", ctypes.c_int32), ("minibatch_count", ctypes.c_int32),
                  ("round_len", ctypes.c_int32), ("epochs", ctypes.c_int32)]
-                + [(n, ctypes.c_void_p) for n in ("reps", "rows", "splits", "x", "labels", "params", "rms", "idx",
+                + [(n, ctypes.c_void_p) for n in ("reps", "rows", "splits", "seq", "x", "labels", "params", "rms", "idx",
                                                    "cnt", "opt_t", "drop_key", "a1", "d2", "code2", "a3", "d4",
                                                    "code4", "d5", "code5", "dh5", "dz4", "dz3", "dz2", "dz1", "wt",
                                                    "wpart")]
@@ -101,6 +101,7 @@ class CifarModel:
         t.n_rep, t.bmax, t.wg_splits = R, B, splits
         t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
         t.reps, t.rows, t.splits = st.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
+        t.seq = st.seq_t.data_ptr() if st.seq_t is not None else None
         t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
         t.params, t.rms = st.params.data_ptr(), st.rms.data_ptr()
         for k, v in st.ws.items():

@@ -29,7 +29,9 @@ W2P = 18496
 WG_SAMPLES = 8
 PATIENCE = 10
 
-REP_IDLE, REP_FEDAVG, REP_SINGLE = -1, 0, 1
+REP_IDLE, REP_FEDAVG, REP_SINGLE, REP_SEQ = -1, 0, 1, 2
+SEQ_REC = 6
+SEQ_APPROACHES = ("seq-pure", "seq-with-final-agg", "seqavg")
 M64 = (1 << 64) - 1
 
 
@@ -51,6 +53,7 @@ class TrainT(ctypes.Structure):
                 ("pad0", ctypes.c_int32), ("step", ctypes.c_int32), ("minibatch_count", ctypes.c_int32),
                 ("round_len", ctypes.c_int32), ("epochs", ctypes.c_int32),
                 ("reps", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("splits", ctypes.c_void_p),
+                ("seq", ctypes.c_void_p),
                 ("x", ctypes.c_void_p), ("labels", ctypes.c_void_p),
                 ("params", ctypes.c_void_p), ("adam_m", ctypes.c_void_p), ("adam_v", ctypes.c_void_p),
                 ("idx", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("adam_t", ctypes.c_void_p),
@@ -102,6 +105,21 @@ def shuffle_key(seed, mask, partner):
     return mix64(mix64(mix64((seed + 0x5EED) & M64) ^ mask) ^ (partner + 1))
 
 
+def seq_order_key(seed, mask):
+    """Key of the per-round member order of a sequential coalition (keyed.h seq_locate)."""
+    return mix64(mix64((seed + 0x5E90) & M64) ^ mask)
+
+
+def _i32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >= (1 << 31) else v
+
+
+def torch_i32(values, device):
+    import torch
+    return torch.tensor(list(values), dtype=torch.int32, device=device)
+
+
 def minibatch_bounds(n, M):
     """[0, int(1/M*n), ..., int((M-1)/M*n), n] exactly as np.split's indices in mplc/partner.py:159-167."""
     split_indices = np.arange(1, M + 1) / M
@@ -148,6 +166,7 @@ class MnistModel:
         t.n_rep, t.bmax, t.w2_splits = R, B, splits
         t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
         t.reps, t.rows, t.splits = st.rep_t.data_ptr(), eng.rows_d.data_ptr(), eng.splits_d.data_ptr()
+        t.seq = st.seq_t.data_ptr() if st.seq_t is not None else None
         t.x, t.labels = eng.x_train_d.data_ptr(), eng.y_train_d.data_ptr()
         t.params, t.adam_m, t.adam_v = st.params.data_ptr(), st.adam_m.data_ptr(), st.adam_v.data_ptr()
         for k, v in st.ws.items():
@@ -200,17 +219,33 @@ class TrainBatch:
         self.stream = _native.stream_handle(dev)
         C = len(coalitions)
         sizes = eng.partner_sizes
-        reps, src, first, single = [], [], [], []
+        self.approach = getattr(eng, "approach", "fedavg")
+        seq_mode = self.approach in SEQ_APPROACHES
+        reps, src, first, single, seq_recs, snap_first = [], [], [], [], [], []
         for ci, coal in enumerate(coalitions):
             mask = sum(1 << p for p in coal)
             first.append(len(reps))
             single.append(len(coal) == 1)
+            if seq_mode and len(coal) > 1:
+                # one model per coalition; member records in ascending partner order (the partners_list order)
+                off = len(seq_recs)
+                for p in coal:
+                    key = shuffle_key(eng.seed, mask, p)
+                    seq_recs.extend([sizes[p], eng.batch_sizes[p], eng.rows_off[p], eng.split_off[p],
+                                     _i32(key & 0xFFFFFFFF), _i32(key >> 32)])
+                snap_first.append(sum(len(coalitions[c]) for c in range(ci) if len(coalitions[c]) > 1))
+                reps.append((REP_SEQ, len(coal), max(eng.batch_sizes[p] for p in coal), off, 0, len(reps),
+                             seq_order_key(eng.seed, mask)))
+                src.append(ci)
+                continue
             for p in coal:
                 reps.append((REP_SINGLE if len(coal) == 1 else REP_FEDAVG, sizes[p], eng.batch_sizes[p],
                              eng.rows_off[p], eng.split_off[p], len(reps), shuffle_key(eng.seed, mask, p)))
                 src.append(ci)
+                snap_first.append(0)
         first.append(len(reps))
         self.coal_first, self.coal_is_single = first, single
+        self.seq_mode = seq_mode
         R = len(reps)
         self.R, self.C = R, C
         self.rep_arr = np.zeros(R, dtype=REPLICA_DTYPE)
@@ -220,13 +255,18 @@ class TrainBatch:
         M = eng.minibatch_count
         round_len, single_steps = 1, 0
         for coal in coalitions:
-            for p in coal:
-                if len(coal) > 1:
+            if len(coal) == 1:
+                p = coal[0]
+                single_steps = max(single_steps, epochs * -(-sizes[p] // eng.batch_sizes[p]))
+            elif seq_mode:  # the members' fits run back to back inside a round
+                for m in range(M):
+                    round_len = max(round_len, sum(-(-(eng.bounds[p][m + 1] - eng.bounds[p][m]) // eng.batch_sizes[p])
+                                                   for p in coal))
+            else:
+                for p in coal:
                     b = eng.bounds[p]
                     for m in range(M):
                         round_len = max(round_len, -(-(b[m + 1] - b[m]) // eng.batch_sizes[p]))
-                else:
-                    single_steps = max(single_steps, epochs * -(-sizes[p] // eng.batch_sizes[p]))
         self.round_len = round_len
         self.fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
         self.total_steps = max(self.fed_steps, single_steps)
@@ -243,6 +283,12 @@ class TrainBatch:
         _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), S,
                                              _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
         self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
+        self.seq_t = torch.tensor(seq_recs, **i32) if seq_recs else None
+        self.snap = None
+        if seq_mode and self.approach != "seq-pure" and seq_recs:
+            # partner.model_weights of the aggregating variants: one snapshot row per (coalition, member)
+            self.snap = torch.zeros((len(seq_recs) // SEQ_REC, S), **f32)
+            self.snap_first_t = torch.tensor(snap_first, **i32)
         self.model.alloc(self)
         self.stopped = np.zeros(C, dtype=bool)
         self.kind_host = self.rep_arr["kind"].copy()
@@ -262,7 +308,16 @@ class TrainBatch:
                 cur.append(ci)
         if cur:
             runs.append(cur)
-        sizes, first = self.eng.partner_sizes, self.coal_first
+        sizes = self.eng.partner_sizes
+        # aggregation inputs: FedAvg replica rows, or the SEQ snapshot rows (members contiguous per coalition)
+        if self.seq_mode:
+            first, acc = [], 0
+            for ci in range(self.C):
+                first.append(acc)
+                acc += len(self.coalitions[ci]) if not self.coal_is_single[ci] else 0
+            first.append(acc)
+        else:
+            first = self.coal_first
         args = []
         for run in runs:
             f = torch.tensor([first[ci] - first[run[0]] for ci in run] + [first[run[-1] + 1] - first[run[0]]],
@@ -272,20 +327,48 @@ class TrainBatch:
                 ww, scl = aggregation_weights([sizes[p] for p in self.coalitions[ci]], self.eng.aggregation)
                 w.extend(ww)
                 sc.append(scl)
-            args.append((first[run[0]], run[0], len(run), f, torch.tensor(w, dtype=torch.float64, device=self.dev),
+            args.append((self.coal_first[run[0]], run[0], len(run), f, torch.tensor(w, dtype=torch.float64, device=self.dev),
                          torch.tensor(sc, dtype=torch.float64, device=self.dev)))
         return args
 
     def step(self, s):
         self.model.step(self, s, self.eng.profiler)
+        if self.snap is not None:
+            t = self.t
+            _native.check(self.lib.mplc_seq_snapshot(_native.ptr(self.params), self.model.STRIDE, self.model.NPARAM,
+                                                     _native.ptr(self.rep_t), self.R, _native.ptr(self.seq_t),
+                                                     ctypes.c_void_p(t.splits), s, t.minibatch_count, t.round_len,
+                                                     t.epochs, _native.ptr(self.snap_first_t), _native.ptr(self.snap),
+                                                     self.stream), "mplc_seq_snapshot")
 
-    def aggregate(self):
+    def _rows_copy(self, dst, src, mapping):
+        m = torch_i32(mapping, self.dev)
+        _native.check(self.lib.mplc_cnn_copy_rows(_native.ptr(dst), _native.ptr(src), self.model.STRIDE, _native.ptr(m),
+                                                  len(mapping), self.stream), "mplc_cnn_copy_rows")
+
+    def aggregate(self, epoch_end=False):
+        """End of a round.  fedavg: data-volume/uniform average of the partner models -> global, broadcast to
+        the replicas (mplc/multi_partner_learning.py:300-311).  seq-pure: the model after the last member is
+        the global model.  seqavg (every round) / seq-with-final-agg (epoch end): average of the members'
+        snapshots -> global -> the coalition model (mplc/multi_partner_learning.py:392-433)."""
         S, NP = self.model.STRIDE, self.model.NPARAM
+        aggregate_now = (not self.seq_mode or self.approach == "seqavg"
+                         or (self.approach == "seq-with-final-agg" and epoch_end))
         for (r0, c0, nc, first, w, sc) in self.run_args:
-            _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(self.params[r0:]), S, _native.ptr(first),
-                                                         _native.ptr(w), _native.ptr(sc), nc, NP,
-                                                         _native.ptr(self.glob[c0:c0 + nc]), S, 1, self.stream),
-                          "mplc_fedavg_aggregate")
+            if aggregate_now:
+                x = self.params[r0:] if not self.seq_mode else self.snap[self.snap_row(c0):]
+                _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(x), S, _native.ptr(first), _native.ptr(w),
+                                                             _native.ptr(sc), nc, NP,
+                                                             _native.ptr(self.glob[c0:c0 + nc]), S,
+                                                             0 if self.seq_mode else 1, self.stream),
+                              "mplc_fedavg_aggregate")
+                if self.seq_mode:  # the averaged model continues training
+                    self._rows_copy(self.params[r0:r0 + nc], self.glob, list(range(c0, c0 + nc)))
+            else:  # sequential without averaging: the coalition model as it stands
+                self._rows_copy(self.glob[c0:c0 + nc], self.params, list(range(r0, r0 + nc)))
+
+    def snap_row(self, ci):
+        return sum(len(self.coalitions[c]) for c in range(ci) if not self.coal_is_single[c])
 
     def stop(self, ci):
         import torch
@@ -348,7 +431,7 @@ class CnnBatchTrainer:
                         val_hist[ci].append(l)
             st.step(s)
             if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
-                st.aggregate()
+                st.aggregate(epoch_end=(s + 1) % per_epoch_fed == 0)
                 if use_es and (s + 1) % per_epoch_fed == 0:
                     e = (s + 1) // per_epoch_fed - 1
                     for ci in fed:

@@ -39,11 +39,15 @@ class CoalitionEngine:
 
     def __init__(self, *, x_train, y_train, x_val, y_val, x_test, y_test, partner_rows, batch_sizes,
                  epoch_count, minibatch_count, aggregation="data-volume", is_early_stopping=True, seed=0,
-                 model="mnist_cnn", device=None, memory_budget_bytes=None, eval_budget_bytes=8 << 30):
+                 model="mnist_cnn", device=None, memory_budget_bytes=None, eval_budget_bytes=8 << 30,
+                 approach="fedavg"):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("MI355X (HIP) device required: the MPLC engine has no CPU fallback")
         self.model_impl = model_class(model)()
+        if approach not in ("fedavg", "seq-pure", "seq-with-final-agg", "seqavg"):
+            raise NotImplementedError(f"multi-partner learning approach '{approach}' has no batched MI355X path")
+        self.approach = approach
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.model = model
         self.seed = int(seed)
@@ -113,6 +117,11 @@ class CoalitionEngine:
                   aggregation=getattr(scenario, "aggregation_weighting", "data-volume"),
                   is_early_stopping=getattr(scenario, "is_early_stopping", True),
                   seed=getattr(scenario, "engine_seed", int(os.environ.get("MPLC_ENGINE_SEED", "0"))), model=model)
+        approach = getattr(getattr(scenario, "multi_partner_learning_approach", None), "engine_approach", "fedavg")
+        if target is cls:
+            kw["approach"] = approach
+        elif approach != "fedavg":
+            raise NotImplementedError(f"'{approach}' is not available for the {name} model (FedAvg only)")
         kw.update(overrides)
         if target is not cls:
             kw.pop("batch_sizes", None)

@@ -114,6 +114,7 @@ class SinglePartnerLearning(MultiPartnerLearning):
 
 class FederatedAverageLearning(MultiPartnerLearning):
     """mplc/multi_partner_learning.py:278-334: FedAvg rounds over minibatches, fresh optimizer per partner fit."""
+    engine_approach = "fedavg"
 
     def __init__(self, scenario, **kwargs):
         super().__init__(scenario, **kwargs)
@@ -121,9 +122,37 @@ class FederatedAverageLearning(MultiPartnerLearning):
             raise ValueError('Only one partner is provided. Please use the dedicated SinglePartnerLearning class')
 
 
+class SequentialLearning(MultiPartnerLearning):
+    """seq-pure, mplc/multi_partner_learning.py:337-381: per round one model (fresh optimizer) trained on
+    each member's minibatch in a shuffled member order; the model after the last member goes on.  On the
+    engine: one MPLC_REP_SEQ replica per coalition (csrc/keyed.h seq_locate)."""
+    engine_approach = "seq-pure"
+
+    def __init__(self, scenario, **kwargs):
+        super().__init__(scenario, **kwargs)
+        if self.partners_count == 1:
+            raise ValueError('Only one partner is provided. Please use the dedicated SinglePartnerLearning class')
+
+
+class SequentialWithFinalAggLearning(SequentialLearning):
+    """seq-with-final-agg, mplc/multi_partner_learning.py:384-405: as seq-pure, and at each epoch end the
+    model is the aggregate of the members' weights after their last fit (csrc/seq.hip snapshots)."""
+    engine_approach = "seq-with-final-agg"
+
+
+class SequentialAverageLearning(SequentialLearning):
+    """seqavg, mplc/multi_partner_learning.py:408-430: as seq-pure, aggregating the members' weights after
+    every round."""
+    engine_approach = "seqavg"
+
+
 MULTI_PARTNER_LEARNING_APPROACHES = {
     "fedavg": FederatedAverageLearning,
+    "seq-pure": SequentialLearning,
+    "seq-with-final-agg": SequentialWithFinalAggLearning,
+    "seqavg": SequentialAverageLearning,
 }
 
-__all__ = ["MultiPartnerLearning", "SinglePartnerLearning", "FederatedAverageLearning",
-           "MULTI_PARTNER_LEARNING_APPROACHES", "operator", "np"]
+__all__ = ["MultiPartnerLearning", "SinglePartnerLearning", "FederatedAverageLearning", "SequentialLearning",
+           "SequentialWithFinalAggLearning", "SequentialAverageLearning", "MULTI_PARTNER_LEARNING_APPROACHES",
+           "operator", "np"]

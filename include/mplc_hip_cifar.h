@@ -76,6 +76,7 @@ typedef struct {
   const mplc_replica_t* reps;
   const int32_t* rows;
   const int32_t* splits;
+  const int32_t* seq;     /* MPLC_REP_SEQ member records (NULL when there are none)        */
   /* data */
   const float* x;         /* [N][32][32][3] fp32 in [0,1]                                 */
   const int32_t* labels;  /* [N] class ids                                                */

@@ -53,6 +53,13 @@ extern "C" {
 #define MPLC_REP_IDLE (-1)
 #define MPLC_REP_FEDAVG 0     /* member of a FedAvg coalition: M rounds per epoch, fresh Adam per round */
 #define MPLC_REP_SINGLE 1     /* singleton coalition: Keras fit over all rows, E epochs, persistent Adam  */
+#define MPLC_REP_SEQ 2        /* sequential coalition model (seq-pure / seq-with-final-agg / seqavg): one
+                               * model per coalition trained on its members' minibatches one after the
+                               * other in a per-round shuffled member order, one optimizer per round
+                               * (mplc/multi_partner_learning.py:337-433).  For this kind n_rows = member
+                               * count k, rows_off = offset of the coalition's k member records in `seq`,
+                               * batch = max member batch size, key = member-order key. */
+#define MPLC_SEQ_REC 6        /* member record in `seq`: n_rows, batch, rows_off, split_off, key lo, key hi */
 
 typedef struct {
   int32_t kind;       /* MPLC_REP_*                                                      */
@@ -78,6 +85,7 @@ typedef struct {
   const mplc_replica_t* reps;
   const int32_t* rows;    /* concatenated partner row indices into x/labels               */
   const int32_t* splits;  /* concatenated minibatch boundaries, M+1 per partner           */
+  const int32_t* seq;     /* MPLC_REP_SEQ member records (NULL when there are none)        */
   /* data */
   const float* x;         /* [N][28][28] fp32 in [0,1]                                    */
   const int32_t* labels;  /* [N] class ids                                                */
@@ -120,6 +128,14 @@ int mplc_cnn_copy_rows(float* dst, const float* src, int64_t stride, const int32
 
 /* Enqueue one lockstep training step of all replicas (schedule, forward, backward, Adam). */
 int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream);
+
+/* Sequential approaches: after step `step`, copy params[r] into snap[snap_first[r] + i] for every
+ * MPLC_REP_SEQ replica r whose member i (ascending partner order) finished its minibatch fit at this step
+ * (partner.model_weights = model.get_weights(), mplc/multi_partner_learning.py:372-374).  The schedule
+ * arguments are those of the train step. */
+int mplc_seq_snapshot(const float* params, int64_t stride, int64_t n_param, const mplc_replica_t* reps, int n_rep,
+                      const int32_t* seq, const int32_t* splits, int step, int minibatch_count, int round_len,
+                      int epochs, const int32_t* snap_first, float* snap, void* stream);
 
 /* Forward-only evaluation of n_models models on samples [0, n_samples) of x/labels:
  * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  pooled/hidden are

@@ -184,7 +184,7 @@ class Data:
 
 
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
-                    aggregation="data-volume", early_stopping=False, return_model=False):
+                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg"):
     """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init, order and masks."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
@@ -220,6 +220,24 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
             if early_stopping and epochs > PATIENCE:
                 val_hist.append(evaluate(glob, data.x_val, data.y_val)[0])
             for m in range(M):
+                if approach != "fedavg":  # sequential approaches, as oracle/cnn.py
+                    params = {k: v.clone() for k, v in glob.items()}
+                    opt = KerasRMSprop(params)
+                    snaps = [None] * len(coalition)
+                    for mi in ocnn.seq_member_order(seed, mask, len(coalition), e, m):
+                        p_id = coalition[mi]
+                        key = ocnn.shuffle_key(seed, mask, p_id)
+                        steps = ocnn.fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m)
+                        for t, rows in enumerate(steps):
+                            masks = step_masks(fedavg_drop_key(key, e, m, t), len(rows))
+                            g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                            opt.step(params, g)
+                        snaps[mi] = {k: v.clone() for k, v in params.items()}
+                    if approach == "seqavg" or (approach == "seq-with-final-agg" and m == M - 1):
+                        glob = ocnn.average_models(glob, snaps, w)
+                    else:
+                        glob = params
+                    continue
                 partner_models = []
                 for p_id in coalition:
                     key = ocnn.shuffle_key(seed, mask, p_id)

@@ -89,6 +89,17 @@ def init_params(key):
     return row
 
 
+def seq_order_key(seed, mask):
+    return mix64(mix64(seed + 0x5E90) ^ mask)
+
+
+def seq_member_order(seed, mask, k, e, m):
+    """Member indices (ascending-partner positions) of a sequential coalition's round (e, m), in the order
+    they train (csrc/keyed.h seq_locate; the reference draws np.random.permutation, :365)."""
+    okey = subkey(seq_order_key(seed, mask), 0x60000 + e, m)
+    return [int(v) for v in keyed_perm(okey, k, np.arange(k))]
+
+
 def minibatch_bounds(n, M):
     split_indices = np.arange(1, M + 1) / M
     return [0] + [int(v) for v in (split_indices[:-1] * n).astype(int)] + [int(n)]
@@ -238,8 +249,18 @@ class Data:
         self.x_test, self.y_test = img(x_test), lab(y_test)
 
 
+def average_models(glob, models, w):
+    """np.average(..., axis=0, weights=w) per layer in float64 -> float32 (mplc/mpl_utils.py:90-102)."""
+    torch = _torch()
+    new = {}
+    for k in glob:
+        stack = np.array([pm[k].numpy() for pm in models])
+        new[k] = torch.from_numpy(np.average(stack, axis=0, weights=w).astype(np.float32))
+    return new
+
+
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
-                    aggregation="data-volume", early_stopping=False, return_model=False):
+                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg"):
     """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init and order."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
@@ -277,6 +298,24 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
             if early_stopping and epochs > PATIENCE:
                 val_hist.append(evaluate(glob, data.x_val, data.y_val)[0])
             for m in range(M):
+                if approach != "fedavg":
+                    # seq-pure / seq-with-final-agg / seqavg (mplc/multi_partner_learning.py:337-433): one model
+                    # and one optimizer per round, members in the round's shuffled order, snapshots per member
+                    params = {k: v.clone() for k, v in glob.items()}
+                    opt = KerasAdam(params)
+                    snaps = [None] * len(coalition)
+                    for mi in seq_member_order(seed, mask, len(coalition), e, m):
+                        p_id = coalition[mi]
+                        key = shuffle_key(seed, mask, p_id)
+                        for rows in fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m):
+                            g, _ = gradients(params, data.x_train[rows], data.y_train[rows])
+                            opt.step(params, g)
+                        snaps[mi] = {k: v.clone() for k, v in params.items()}
+                    if approach == "seqavg" or (approach == "seq-with-final-agg" and m == M - 1):
+                        glob = average_models(glob, snaps, w)
+                    else:
+                        glob = params
+                    continue
                 partner_models = []
                 for p_id in coalition:
                     key = shuffle_key(seed, mask, p_id)
@@ -286,11 +325,7 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                         g, _ = gradients(params, data.x_train[rows], data.y_train[rows])
                         opt.step(params, g)
                     partner_models.append(params)
-                new = {}
-                for k in glob:  # np.average(..., axis=0, weights=w) in float64 -> float32 (mplc/mpl_utils.py:96-100)
-                    stack = np.array([pm[k].numpy() for pm in partner_models])
-                    new[k] = torch.from_numpy(np.average(stack, axis=0, weights=w).astype(np.float32))
-                glob = new
+                glob = average_models(glob, partner_models, w)
             if early_stopping and epochs > PATIENCE and e >= PATIENCE and val_hist[e] > val_hist[e - PATIENCE]:
                 epochs_done = e + 1
                 break

@@ -1,0 +1,134 @@
+"""GPU parity of the sequential multi-partner approaches (seq-pure, seq-with-final-agg, seqavg;
+mplc/multi_partner_learning.py:337-433) on the batched trainers against the oracles.
+
+Bit-exact: the per-step member, sample rows and optimizer iteration of a sequential coalition (keyed member
+order per round), the per-member snapshots and their np.average.  Floating point: trained accuracies
+within +-1 point on average of the oracle (each within 3 points), MNIST and CIFAR10 models."""
+import numpy as np
+import pytest
+
+from oracle import cnn as ocnn
+
+pytestmark = pytest.mark.gpu
+
+APPROACHES = ("seq-pure", "seq-with-final-agg", "seqavg")
+
+
+def make_scenario(approach, cifar=False, partners=3, amounts=(0.2, 0.5, 0.3), M=2, G=4, E=2):
+    from mplc.dataset import ArrayDataset, digits_as_cifar, digits_as_mnist
+    from mplc.scenario import Scenario
+    x, y = digits_as_cifar() if cifar else digits_as_mnist()
+    ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:], name="cifar10" if cifar else "mnist")
+    sc = Scenario(partners, list(amounts), dataset=ds, minibatch_count=M, gradient_updates_per_pass_count=G,
+                  epoch_count=E, is_early_stopping=False, multi_partner_learning_approach=approach)
+    return sc.provision()
+
+
+def engine_for(sc):
+    from mplc.engine import CoalitionEngine
+    return CoalitionEngine.for_scenario(sc, memory_budget_bytes=16 << 30, eval_budget_bytes=1 << 30)
+
+
+def test_sequential_schedule_bit_exact():
+    import torch
+    sc = make_scenario("seqavg")
+    eng = engine_for(sc)
+    assert eng.approach == "seqavg"
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    coal = (0, 1, 2)
+    st = eng.trainer.prepare([coal, (1,)], 2)
+    assert st.R == 2 and st.seq_mode
+    M = eng.minibatch_count
+    mask = 0b111
+    for e in range(2):
+        for m in range(M):
+            expect = []  # (member, rows) per step of this round, in the keyed member order
+            for mi in ocnn.seq_member_order(eng.seed, mask, 3, e, m):
+                p = coal[mi]
+                for rows in ocnn.fedavg_round_rows(ocnn.shuffle_key(eng.seed, mask, p), prow[p], bs[p], M, e, m):
+                    expect.append(rows)
+            assert len(expect) <= st.round_len
+            for t in (0, 1, len(expect) - 1, st.round_len - 1):
+                s = (e * M + m) * st.round_len + t
+                st.step(s)
+                torch.cuda.synchronize()
+                cnt = st.ws["cnt"].cpu().numpy()
+                idx = st.ws["idx"].cpu().numpy()
+                at = st.ws["adam_t"].cpu().numpy()
+                if t < len(expect):
+                    assert cnt[0] == len(expect[t]) and at[0] == t + 1
+                    assert idx[0, :cnt[0]].tolist() == [int(v) for v in expect[t]]
+                else:
+                    assert cnt[0] == 0
+
+
+def test_seqavg_snapshots_and_average_exact():
+    import torch
+    sc = make_scenario("seqavg")
+    eng = engine_for(sc)
+    st = eng.trainer.prepare([(0, 1, 2)], 1)
+    M = eng.minibatch_count
+    order = ocnn.seq_member_order(eng.seed, 0b111, 3, 0, 0)
+    p_after = {}
+    for s in range(st.round_len):
+        st.step(s)
+        torch.cuda.synchronize()
+        p_after[s] = st.params[0].cpu().numpy().copy()
+    snaps = st.snap.cpu().numpy()
+    # member mi's snapshot is the model right after its last step
+    steps = [len(ocnn.fedavg_round_rows(ocnn.shuffle_key(eng.seed, 0b111, p), sc.partners_list[p].train_idx,
+                                        sc.partners_list[p].batch_size, M, 0, 0)) for p in (0, 1, 2)]
+    end = -1
+    for mi in order:
+        end += steps[mi]
+        assert np.array_equal(snaps[mi], p_after[end])
+    st.aggregate(epoch_end=False)
+    torch.cuda.synchronize()
+    sizes = [eng.partner_sizes[p] for p in (0, 1, 2)]
+    ref = np.average(snaps[:, :ocnn.STRIDE], axis=0, weights=np.asarray(sizes) / np.sum(sizes)).astype(np.float32)
+    assert np.array_equal(st.glob.cpu().numpy()[0], ref)
+    assert np.array_equal(st.params.cpu().numpy()[0], ref)  # the averaged model continues
+
+
+@pytest.mark.parametrize("approach", APPROACHES)
+def test_mnist_sequential_accuracies_vs_oracle(approach):
+    sc = make_scenario(approach)
+    eng = engine_for(sc)
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    ds = sc.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    coals = [(0, 1), (1, 2), (0, 1, 2)]
+    dev = eng.evaluate(coals)
+    ref = np.array([ocnn.coalition_value(data, prow, bs, c, seed=eng.seed, epochs=eng.epoch_count,
+                                         M=eng.minibatch_count, approach=approach)[0] for c in coals])
+    diff = np.abs(dev - ref)
+    assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
+    assert np.all(dev > 0.5)
+
+
+@pytest.mark.parametrize("approach", ("seq-pure", "seqavg"))
+def test_cifar_sequential_accuracies_vs_oracle(approach):
+    from oracle import cifar_cnn as occ
+    sc = make_scenario(approach, cifar=True)
+    eng = engine_for(sc)
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    ds = sc.dataset
+    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    coals = [(0, 1), (0, 1, 2)]
+    dev = eng.evaluate(coals)
+    ref = np.array([occ.coalition_value(data, prow, bs, c, seed=eng.seed, epochs=eng.epoch_count,
+                                        M=eng.minibatch_count, approach=approach)[0] for c in coals])
+    diff = np.abs(dev - ref)
+    assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
+
+
+def test_scenario_run_with_sequential_approach_and_shapley():
+    sc = make_scenario("seq-with-final-agg", E=1)
+    sc.methods = ["Shapley values"]
+    sc.run()
+    assert sc.mpl.history.score > 0.5
+    sv = sc.contributivity_list[0]
+    assert abs(np.sum(sv.contributivity_scores) - sc.mpl.history.score) < 1e-9
