@@ -13,6 +13,7 @@
 // Work is tiny (28 unknowns, tens of rows): latency-bound; the point is doing all coalitions in ONE launch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "keyed.h"
 #include "mplc_hip.h"
 
 namespace {
@@ -21,33 +22,6 @@ constexpr int LR_THREADS = 256;
 constexpr int LR_MAXF = 64;   // features (+1 intercept) supported
 constexpr int LR_MAXP = 64;   // partners per coalition
 constexpr int LR_CHUNK = 2048; // rows whose sigma is staged in LDS at a time
-
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t subkey(uint64_t key, uint32_t a, uint32_t b) {
-  return mix64(key ^ mix64(((uint64_t)a << 32) | (uint64_t)b));
-}
-__device__ __forceinline__ uint32_t keyed_perm(uint64_t key, uint32_t n, uint32_t i) {
-  if (n <= 1) return 0;
-  const int bits = 32 - __clz(n - 1);
-  const int h = (bits + 1) >> 1;
-  const uint32_t mask = (1u << h) - 1u;
-  uint32_t x = i;
-  do {
-    uint32_t L = x >> h, R = x & mask;
-    for (int rd = 0; rd < 4; ++rd) {
-      const uint32_t F = (uint32_t)mix64(key ^ ((uint64_t)rd << 40) ^ (uint64_t)R) & mask;
-      const uint32_t nl = R;
-      R = L ^ F;
-      L = nl;
-    }
-    x = (L << h) | R;
-  } while (x >= n);
-  return x;
-}
 
 struct Shared {
   double theta[LR_MAXF];
