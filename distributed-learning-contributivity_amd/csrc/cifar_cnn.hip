@@ -51,9 +51,24 @@ constexpr float SCALE_25 = 0x1.555556p+0f;  // float(1 / 0.75)
 constexpr float SCALE_50 = 2.0f;
 constexpr uint8_t CODE_KEEP = 0x40, CODE_POS = 0x80;
 
-__device__ __forceinline__ bool drop_keep(uint64_t dkey, uint32_t layer, uint32_t j, uint32_t e, uint32_t thr) {
-  const uint64_t h = mix64(dkey ^ mix64(((uint64_t)layer << 56) | ((uint64_t)j << 32) | (uint64_t)e));
-  return (uint32_t)(h >> 40) >= thr;
+// 32-bit finaliser (lowbias32): a bijection with full avalanche; 2 multiplies, cheap next to the 64-bit mix.
+__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// keep(element e) = top 24 bits of hash32(row_seed ^ e) >= rate * 2^24, row_seed = drop_row_seed(step key,
+// layer, slot j): one hash per element (restated in oracle/cifar_cnn.py).
+__device__ __forceinline__ uint32_t drop_row_seed(uint64_t dkey, uint32_t layer, uint32_t j) {
+  return hash32((uint32_t)dkey ^ hash32((uint32_t)(dkey >> 32) ^ (layer << 24) ^ j));
+}
+
+__device__ __forceinline__ bool drop_keep(uint32_t row_seed, uint32_t e, uint32_t thr) {
+  return (hash32(row_seed ^ e) >> 8) >= thr;
 }
 
 __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
@@ -195,21 +210,30 @@ struct ConvArgs {
   uint8_t* code_out;         // pooled forward, train
 };
 
-__host__ __device__ constexpr int ci3_off(int k, int wip) { return ((k / 9) * wip + (k / 3) % 3) * 3 + k % 3; }
+// LDS offset of K index k = (ky*3 + kx)*3 + c of the 3-channel input (row stride rowp, pixel stride 3)
+__host__ __device__ constexpr int ci3_off(int k, int rowp) { return (k / 9) * rowp + ((k / 3) % 3) * 3 + k % 3; }
 
+// M tiles are 2-D: a 32-row tile is a 4 x 8 block of output pixels, or for the pooled forward a 2 x 4 block
+// of pool windows with lane m = window * 4 + q (so the 4 pixels of a window are accumulator registers
+// 4g..4g+3 of one lane: the pool is a register max).  With the LDS row stride = 8 (mod 32) dwords and an
+// odd pixel stride, the 32 pixels of a tile fall on 32 distinct banks.
 template <int HI, int WI, int CI, int CO, int PAD, int BR, int NW, int UM, int EPI>
 __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
   constexpr int PH = HO / 2, PW = WO / 2;
-  constexpr int ROWS = POOL ? 2 * BR : BR;  // output rows per band
+  constexpr int ROWS = POOL ? 2 * BR : BR;  // output rows per band (BR window rows when pooled)
+  constexpr int TX = POOL ? (PW + 3) / 4 : (WO + 7) / 8;
+  constexpr int TY = POOL ? BR / 2 : BR / 4;
+  constexpr int TILES = TX * TY;
   constexpr int LR = ROWS + 2, WIP = WI + 2 * PAD, CIP = CI | 1;
+  constexpr int ROWP = WIP * CIP + ((8 - (WIP * CIP) % 32) + 32) % 32;
   constexpr int NT = CO / 32;
-  constexpr int MROWS = POOL ? BR * PW * 4 : BR * WO;
   constexpr int NTHR = NW * 64;
-  static_assert(NW * UM * 32 >= MROWS, "row tiles do not cover the band");
-  static_assert(CO % 32 == 0 && (CI == 3 || CI % 2 == 0), "unsupported channel counts");
-  __shared__ float in_s[LR * WIP * CIP];
+  static_assert(POOL ? BR % 2 == 0 : BR % 4 == 0, "bands are whole tile rows");
+  static_assert(NW * UM >= TILES, "row tiles do not cover the band");
+  static_assert(CO % 32 == 0 && (CI == 3 || CI % 4 == 0), "unsupported channel counts");
+  __shared__ float in_s[LR * ROWP];
   const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
   if (j >= count) return;
@@ -220,36 +244,61 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
                      : a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ
                                       : a.in + slot * IN_SZ;
   const int y0 = band * ROWS;
-  for (int e = tid; e < LR * WIP * CI; e += NTHR) {
-    const int c = e % CI;
-    const int col = (e / CI) % WIP;
-    const int rr = e / (CI * WIP);
-    const int iy = y0 - PAD + rr, ix = col - PAD;
-    float v = 0.0f;
-    if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
-    in_s[(rr * WIP + col) * CIP + c] = v;
+  if constexpr (CI % 4 == 0) {
+    // 16-B loads along the channels; each thread keeps one channel quad and walks pixels incrementally
+    constexpr int C4 = CI / 4;
+    static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
+    constexpr int PSTEP = NTHR / C4;
+    const int c4 = tid % C4;
+    int pix = tid / C4;
+    int rr = pix / WIP, col = pix % WIP;
+    for (; pix < LR * WIP; pix += PSTEP) {
+      const int iy = y0 - PAD + rr, ix = col - PAD;
+      fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
+        v = *reinterpret_cast<const fvec4*>(src + (iy * WI + ix) * CI + 4 * c4);
+      float* d = in_s + rr * ROWP + col * CIP + 4 * c4;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+      col += PSTEP % WIP;
+      rr += PSTEP / WIP;
+      if (col >= WIP) { col -= WIP; ++rr; }
+    }
+  } else {
+    for (int e = tid; e < LR * WIP * CI; e += NTHR) {
+      const int c = e % CI;
+      const int col = (e / CI) % WIP;
+      const int rr = e / (CI * WIP);
+      const int iy = y0 - PAD + rr, ix = col - PAD;
+      float v = 0.0f;
+      if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
+      in_s[rr * ROWP + col * CIP + c] = v;
+    }
   }
   const int lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31, kh = lane >> 5;
   int abase[UM];
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
-    const int p = (wave + NW * u) * 32 + n;
+    const int t = wave + NW * u;
+    const int ty = t / TX, tx = t % TX;
     int yl, x;
     bool ok;
     if (POOL) {
-      const int w = p >> 2, q = p & 3;
-      const int pyl = w / PW;
-      yl = 2 * pyl + (q >> 1);
-      x = 2 * (w % PW) + (q & 1);
-      ok = p < MROWS && band * BR + pyl < PH;
+      const int wi = n >> 2, q = n & 3;
+      const int wy = ty * 2 + wi / 4, wx = tx * 4 + wi % 4;
+      yl = 2 * wy + (q >> 1);
+      x = 2 * wx + (q & 1);
+      ok = t < TILES && wx < PW && band * BR + wy < PH;
     } else {
-      yl = p / WO;
-      x = p % WO;
-      ok = p < MROWS && y0 + yl < HO;
+      yl = ty * 4 + n / 8;
+      x = tx * 8 + n % 8;
+      ok = t < TILES && x < WO && y0 + yl < HO;
     }
     if (!ok) { yl = 0; x = 0; }
-    abase[u] = (yl * WIP + x) * CIP + (CI == 3 ? 0 : kh);
+    abase[u] = yl * ROWP + x * CIP + (CI == 3 ? 0 : kh);
   }
   floatx16 acc[UM][NT];
 #pragma unroll
@@ -264,7 +313,7 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
 #pragma unroll
     for (int s = 0; s < 14; ++s) {
       const bool valid = (2 * s + kh) < 27;
-      const int off = kh ? (2 * s + 1 < 27 ? ci3_off(2 * s + 1, WIP) : 0) : ci3_off(2 * s, WIP);
+      const int off = kh ? (2 * s + 1 < 27 ? ci3_off(2 * s + 1, ROWP) : 0) : ci3_off(2 * s, ROWP);
       const float b = valid ? Wl[2 * s * CO] : 0.0f;
 #pragma unroll
       for (int u = 0; u < UM; ++u) {
@@ -275,7 +324,7 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
   } else {
 #pragma unroll
     for (int kyx = 0; kyx < 9; ++kyx) {
-      const int offA = ((kyx / 3) * WIP + kyx % 3) * CIP;
+      const int offA = (kyx / 3) * ROWP + (kyx % 3) * CIP;
       const float* Wk = W + (int64_t)(kyx * CI + kh) * CO + n;
 #pragma unroll
       for (int c2 = 0; c2 < CI / 2; ++c2) {
@@ -291,39 +340,25 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
       }
     }
   }
-  // ---- epilogues ----
-  if constexpr (EPI == EPI_FWD) {
-    const float* bias = a.bias + (int64_t)r * a.b_rstride;
-    float* o = a.out + slot * (HO * WO * CO);
-#pragma unroll
-    for (int u = 0; u < UM; ++u)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const float bv = bias[nt * 32 + n];
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
-          const int y = y0 + p / WO, x = p % WO;
-          if (p < MROWS && y < HO) o[(y * WO + x) * CO + nt * 32 + n] = fmaxf(acc[u][nt][reg] + bv, 0.0f);
-        }
-      }
-  } else if constexpr (EPI == EPI_FWD_POOL) {
+  // ---- epilogues: accumulator register -> tile row rt = acc_row(reg, kh) -> pixel / window ----
+  if constexpr (EPI == EPI_FWD_POOL) {
     const float* bias = a.bias + (int64_t)r * a.b_rstride;
     float* o = a.out + slot * (PH * PW * CO);
     uint8_t* oc = a.drop_key ? a.code_out + slot * (PH * PW * CO) : nullptr;
-    const uint64_t dkey = a.drop_key ? a.drop_key[r] : 0ull;
+    const uint32_t rseed = a.drop_key ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
 #pragma unroll
-    for (int u = 0; u < UM; ++u)
+    for (int u = 0; u < UM; ++u) {
+      const int t = wave + NW * u;
+      const int ty = t / TX, tx = t % TX;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = nt * 32 + n;
         const float bv = bias[co];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int wl = (wave + NW * u) * 8 + 2 * g + kh;
-          const int pyl = wl / PW, px = wl % PW;
-          const int py = band * BR + pyl;
-          if (wl * 4 < MROWS && py < PH) {
+          const int wi = 2 * g + kh;
+          const int py = band * BR + ty * 2 + wi / 4, px = tx * 4 + wi % 4;
+          if (t < TILES && px < PW && ty * 2 + wi / 4 < BR && py < PH) {
             float best = acc[u][nt][4 * g] + bv;
             int arg = 0;
 #pragma unroll
@@ -334,7 +369,7 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
             const int pidx = (py * PW + px) * CO + co;
             const float av = fmaxf(best, 0.0f);
             if (oc) {
-              const bool keep = drop_keep(dkey, a.drop_layer, (uint32_t)j, (uint32_t)pidx, THR_25);
+              const bool keep = drop_keep(rseed, (uint32_t)pidx, THR_25);
               o[pidx] = keep ? av * SCALE_25 : 0.0f;
               oc[pidx] = (uint8_t)(arg | (keep ? CODE_KEEP : 0) | (best > 0.0f ? CODE_POS : 0));
             } else {
@@ -343,44 +378,43 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
           }
         }
       }
-  } else if constexpr (EPI == EPI_BWD_MASK) {
-    const float* act = a.aux + slot * (HO * WO * CO);
-    float* o = a.out + slot * (HO * WO * CO);
+    }
+  } else {
+    const float* bias = (EPI == EPI_FWD) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
+    const float* act = (EPI == EPI_BWD_MASK) ? a.aux + slot * (HO * WO * CO) : nullptr;
+    const uint8_t* cd = (EPI == EPI_BWD_UNPOOL) ? a.code_in + slot * (HO * WO * CO) : nullptr;
+    float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * HO * WO * CO);
 #pragma unroll
-    for (int u = 0; u < UM; ++u)
+    for (int u = 0; u < UM; ++u) {
+      const int t = wave + NW * u;
+      const int ty = t / TX, tx = t % TX;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
-          const int y = y0 + p / WO, x = p % WO;
-          if (p < MROWS && y < HO) {
-            const int o_i = (y * WO + x) * CO + nt * 32 + n;
-            o[o_i] = act[o_i] > 0.0f ? acc[u][nt][reg] : 0.0f;
-          }
-        }
-  } else {  // EPI_BWD_UNPOOL: grid = pooled+dropout grid of the layer below; out = its dense dZ (2HO x 2WO)
-    const uint8_t* cd = a.code_in + slot * (HO * WO * CO);
-    float* o = a.out + slot * (4 * HO * WO * CO);
-#pragma unroll
-    for (int u = 0; u < UM; ++u)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
+      for (int nt = 0; nt < NT; ++nt) {
+        const int ch = nt * 32 + n;
+        const float bv = (EPI == EPI_FWD) ? bias[ch] : 0.0f;
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-          const int p = (wave + NW * u) * 32 + acc_row(reg, kh);
-          const int y = y0 + p / WO, x = p % WO;
-          if (p < MROWS && y < HO) {
-            const int ch = nt * 32 + n;
-            const uint32_t c = cd[(y * WO + x) * CO + ch];
-            const float v = (c & CODE_KEEP) ? acc[u][nt][reg] * SCALE_25 : 0.0f;
+          const int rt = acc_row(reg, kh);
+          const int y = y0 + ty * 4 + rt / 8, x = tx * 8 + rt % 8;
+          if (!(t < TILES && x < WO && y < HO)) continue;
+          const int o_i = (y * WO + x) * CO + ch;
+          const float v = acc[u][nt][reg];
+          if constexpr (EPI == EPI_FWD) {
+            o[o_i] = fmaxf(v + bv, 0.0f);
+          } else if constexpr (EPI == EPI_BWD_MASK) {
+            o[o_i] = act[o_i] > 0.0f ? v : 0.0f;
+          } else {  // dropout' + un-pool into the dense dZ (2HO x 2WO) of the layer below
+            const uint32_t c = cd[o_i];
+            const float dv = (c & CODE_KEEP) ? v * SCALE_25 : 0.0f;
             const bool pos = (c & CODE_POS) != 0;
             const int sel = c & 3;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              o[((2 * y + (q >> 1)) * (2 * WO) + 2 * x + (q & 1)) * CO + ch] = (pos && sel == q) ? v : 0.0f;
+              o[((2 * y + (q >> 1)) * (2 * WO) + 2 * x + (q & 1)) * CO + ch] = (pos && sel == q) ? dv : 0.0f;
           }
         }
+      }
+    }
   }
 }
 
@@ -420,11 +454,11 @@ __global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
   constexpr int RW = KSPLIT ? BR / NW : BR;  // rows of the band per wave
   constexpr int SW = RW * WOE / 2;           // k-steps per wave per band
   static_assert(KSPLIT ? (BR % NW == 0 && NT == 1) : (MT % NW == 0), "bad wave split");
-  static_assert(NTHR % CO == 0, "db accumulation needs a fixed channel per thread");
+  static_assert(NTHR % (CO / 4) == 0, "db accumulation needs a fixed channel quad per thread");
   static_assert(!KSPLIT || NW * 1024 <= BR * WOE * CO, "reduction scratch aliases the dZ band");
   __shared__ float x_s[(BR + 2) * WXP * CI];
   __shared__ float z_s[BR * WOE * CO];
-  __shared__ float gb_s[NTHR];
+  __shared__ fvec4 gb_s[NTHR];
   const int sp = blockIdx.x, r = blockIdx.y;
   const int count = a.cnt[r];
   const int j_begin = sp * WGS, j_end = min(count, j_begin + WGS);
@@ -457,7 +491,7 @@ __global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
   for (int u = 0; u < UMW; ++u)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[u][nt] = zero16();
-  float gb = 0.0f;
+  fvec4 gb = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // db partial of channels 4*(tid % (CO/4)) .. +3
   for (int j = j_begin; j < j_end; ++j) {
     const int64_t slot = (int64_t)r * a.bmax + j;
     const float* X = a.x_mode == 1 ? a.x + (int64_t)a.idx[slot] * (HI * WI * CI) : a.x + slot * (HI * WI * CI);
@@ -465,20 +499,45 @@ __global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
     for (int band = 0; band < NB; ++band) {
       const int y0 = band * BR;
       __syncthreads();  // previous band's readers done
-      for (int e = tid; e < (BR + 2) * WXP * CI; e += NTHR) {
-        const int c = e % CI;
-        const int col = (e / CI) % WXP;
-        const int rr = e / (CI * WXP);
-        const int iy = y0 - PAD + rr, ix = col - PAD;
-        x_s[e] = (iy >= 0 && iy < HI && ix >= 0 && ix < WI) ? X[(iy * WI + ix) * CI + c] : 0.0f;
+      if constexpr (CI % 4 == 0) {  // 16-B loads and ds_write_b128, incremental pixel walk
+        constexpr int C4 = CI / 4, PSTEP = NTHR / C4;
+        static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
+        const int c4 = tid % C4;
+        int pix = tid / C4;
+        int rr = pix / WXP, col = pix % WXP;
+        for (; pix < (BR + 2) * WXP; pix += PSTEP) {
+          const int iy = y0 - PAD + rr, ix = col - PAD;
+          fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+          if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
+            v = *reinterpret_cast<const fvec4*>(X + (iy * WI + ix) * CI + 4 * c4);
+          *reinterpret_cast<fvec4*>(x_s + pix * CI + 4 * c4) = v;
+          col += PSTEP % WXP;
+          rr += PSTEP / WXP;
+          if (col >= WXP) { col -= WXP; ++rr; }
+        }
+      } else {
+        for (int e = tid; e < (BR + 2) * WXP * CI; e += NTHR) {
+          const int c = e % CI;
+          const int col = (e / CI) % WXP;
+          const int rr = e / (CI * WXP);
+          const int iy = y0 - PAD + rr, ix = col - PAD;
+          x_s[e] = (iy >= 0 && iy < HI && ix >= 0 && ix < WI) ? X[(iy * WI + ix) * CI + c] : 0.0f;
+        }
       }
-      for (int e = tid; e < BR * WOE * CO; e += NTHR) {
-        const int c = e % CO;
-        const int xx = (e / CO) % WOE;
-        const int yy = y0 + e / (CO * WOE);
-        const float v = (yy < HOV && xx < WOV) ? Z[(yy * WO + xx) * CO + c] : 0.0f;
-        z_s[e] = v;
-        gb += v;
+      {
+        constexpr int Z4 = CO / 4, PSTEP = NTHR / Z4;  // each thread: one channel quad of dZ (db too)
+        int pix = tid / Z4;
+        int yy = pix / WOE, xx = pix % WOE;
+        for (; pix < BR * WOE; pix += PSTEP) {
+          fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+          if (y0 + yy < HOV && xx < WOV)
+            v = *reinterpret_cast<const fvec4*>(Z + ((y0 + yy) * WO + xx) * CO + 4 * (tid % Z4));
+          *reinterpret_cast<fvec4*>(z_s + pix * CO + 4 * (tid % Z4)) = v;
+          gb += v;
+          xx += PSTEP % WOE;
+          yy += PSTEP / WOE;
+          if (xx >= WOE) { xx -= WOE; ++yy; }
+        }
       }
       __syncthreads();
 #pragma unroll
@@ -525,9 +584,10 @@ __global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
     }
     __syncthreads();
   }
-  if (tid < CO) {
+  if (tid < CO) {  // channel tid: quad tid/4 of threads tid/4 + (CO/4)*i, summed in thread order
+    constexpr int Z4 = CO / 4;
     float s = 0.0f;
-    for (int i = 0; i < NTHR / CO; ++i) s += gb_s[tid + CO * i];
+    for (int i = 0; i < NTHR / Z4; ++i) s += gb_s[tid / 4 + Z4 * i][tid % 4];
     out[a.off_b + tid] = s;
   }
 }
@@ -603,7 +663,7 @@ __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict
       const float h = fmaxf(z, 0.0f);
       const int64_t o = ((int64_t)r * bmax + row) * HID + col;
       if (drop_key) {
-        const bool keep = drop_keep(dkey, DROP_L5, (uint32_t)row, (uint32_t)col, THR_50);
+        const bool keep = drop_keep(drop_row_seed(dkey, DROP_L5, (uint32_t)row), (uint32_t)col, THR_50);
         H[o] = keep ? h * SCALE_50 : 0.0f;
         code[o] = (uint8_t)((keep ? CODE_KEEP : 0) | (z > 0.0f ? CODE_POS : 0));
       } else {
@@ -708,90 +768,132 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense(512) backward + RMSprop, per 16-row slice of W5 (16 threads per row, 8 fvec4 each):
+// Dense(512) backward + RMSprop, per 32-row slice of W5, 8 rows at a time (32 threads per row, 4 fvec4
+// each: every access instruction covers 512 contiguous bytes of a row); dh5 is staged in LDS once per
+// block for its 4 row groups:
 //   dd4[j][k] = sum_n dh5[j][n] W5[k][n];  dW5[k][n] = sum_j d4[j][k] dh5[j][n];  db5 (slice-0 block).
 // dd4 goes through dropout'(.25) and the 2x2 pool (argmax + relu' from code4) into the dense dz4.
+// HBM-bound: W5 and its accumulator are read and written once per step (the accumulator is not read on a
+// fresh optimizer's first step).
 // ------------------------------------------------------------------------------------------------
-constexpr int D5_ROWS = 16;
-constexpr int D5_SCHUNK = 16;
+constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
+constexpr int D5_GROUPS = 4;    // row groups per block
+constexpr int D5_SCHUNK = 16;   // samples staged at a time
 
 __global__ __launch_bounds__(256) void dense5_bwd_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
     const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
     float* __restrict__ rms, float* __restrict__ dZ4, float lr, float rho, float omr, float decay, float eps) {
+  constexpr int KB = D5_ROWS * D5_GROUPS;
   __shared__ fvec4 dh_s[D5_SCHUNK * (HID / 4)];
-  __shared__ float p_s[D5_SCHUNK * D5_ROWS];
+  __shared__ float p_s[D5_SCHUNK * KB];
+  __shared__ uint8_t c_s[D5_SCHUNK * KB];
   const int r = blockIdx.y;
-  const int k0 = blockIdx.x * D5_ROWS;
+  const int kb = blockIdx.x * KB;
   const int count = cnt[r];
   if (count == 0) return;
   const int tid = threadIdx.x;
-  const int rowl = tid >> 4;
-  const int c16 = tid & 15;
+  const int rowl = tid >> 5;
+  const int c32 = tid & 31;
   const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
-  const int64_t roff = (int64_t)r * STRIDE + OFF_W5 + (int64_t)(k0 + rowl) * HID;
-  fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c16;
-  fvec4* Ra = reinterpret_cast<fvec4*>(rms + roff) + c16;
-  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  fvec4 w[8], g[8], av[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    w[i] = W[16 * i];
-    g[i] = z4;
-    av[i] = z4;
-  }
-  if (!cfg.reset) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) av[i] = __builtin_nontemporal_load(Ra + 16 * i);
-  }
-  const int k = k0 + rowl;
-  const int pix = k / 64, ch = k % 64;
-  const int py = pix / 6, px = pix % 6;
   const float* Pr = D4 + (int64_t)r * bmax * FEAT;
+  const uint8_t* Cr = code4 + (int64_t)r * bmax * FEAT;
   const fvec4* dHr = reinterpret_cast<const fvec4*>(dH + (int64_t)r * bmax * HID);
-  for (int c0 = 0; c0 < count; c0 += D5_SCHUNK) {
-    const int cn = min(D5_SCHUNK, count - c0);
+  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  // staged per sample chunk: dh5 rows, the block's 32 d4 values and their pool/dropout codes
+  auto stage = [&](int c0, int cn) {
     for (int e = tid; e < cn * (HID / 4); e += 256) dh_s[e] = dHr[(int64_t)c0 * (HID / 4) + e];
-    for (int e = tid; e < cn * D5_ROWS; e += 256) {
-      const int jj = e / D5_ROWS, kk = e % D5_ROWS;
-      p_s[e] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + kk];
+    for (int e = tid; e < cn * KB; e += 256) {
+      const int64_t g = (int64_t)(c0 + e / KB) * FEAT + kb + e % KB;
+      p_s[e] = Pr[g];
+      c_s[e] = Cr[g];
     }
-    __syncthreads();
-    for (int jj = 0; jj < cn; ++jj) {
-      const float pv = p_s[jj * D5_ROWS + rowl];
-      float d = 0.0f;
+  };
+  const bool one_chunk = count <= D5_SCHUNK;  // the usual case: staged once for all row groups
+  auto row_ptrs = [&](int grp, fvec4*& W, fvec4*& Ra) {
+    const int64_t roff = (int64_t)r * STRIDE + OFF_W5 + (int64_t)(kb + grp * D5_ROWS + rowl) * HID;
+    W = reinterpret_cast<fvec4*>(params + roff) + c32;
+    Ra = reinterpret_cast<fvec4*>(rms + roff) + c32;
+  };
+  // software pipeline: the next row group's W5 / accumulator loads are in flight while this one computes
+  fvec4 w[4], av[4], wn[4], avn[4];
+  fvec4 *W, *Ra;
+  row_ptrs(0, W, Ra);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const fvec4 dh = dh_s[jj * (HID / 4) + c16 + 16 * i];
-        g[i].x += pv * dh.x; g[i].y += pv * dh.y; g[i].z += pv * dh.z; g[i].w += pv * dh.w;
-        d += dh.x * w[i].x; d += dh.y * w[i].y; d += dh.z * w[i].z; d += dh.w * w[i].w;
-      }
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      d += __shfl_xor(d, 8, 64);
-      if (c16 < 4) {  // un-pool: lane c16 = q writes window pixel q
-        const int64_t slot = (int64_t)r * bmax + c0 + jj;
-        const uint32_t c = code4[slot * FEAT + k];
-        const float v = (c & CODE_KEEP) ? d * SCALE_25 : 0.0f;
-        const bool hit = (c & CODE_POS) && (int)(c & 3) == c16;
-        dZ4[slot * MPLC_CIFAR_DZ4 + ((2 * py + (c16 >> 1)) * 13 + 2 * px + (c16 & 1)) * 64 + ch] = hit ? v : 0.0f;
-      }
-    }
+  for (int i = 0; i < 4; ++i) {
+    w[i] = W[32 * i];
+    av[i] = cfg.reset ? z4 : __builtin_nontemporal_load(Ra + 32 * i);
+  }
+  if (one_chunk) {
+    stage(0, count);
     __syncthreads();
   }
+  for (int grp = 0; grp < D5_GROUPS; ++grp) {
+    fvec4 *Wn = W, *Ran = Ra;
+    if (grp + 1 < D5_GROUPS) {
+      row_ptrs(grp + 1, Wn, Ran);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    fvec4 pw = w[i];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float p1 = pw[q], a1 = av[i][q];
-      rms_apply(p1, a1, g[i][q], cfg);
-      pw[q] = p1;
-      av[i][q] = a1;
+      for (int i = 0; i < 4; ++i) {
+        wn[i] = Wn[32 * i];
+        avn[i] = cfg.reset ? z4 : __builtin_nontemporal_load(Ran + 32 * i);
+      }
     }
-    W[16 * i] = pw;
-    __builtin_nontemporal_store(av[i], Ra + 16 * i);
+    const int k = kb + grp * D5_ROWS + rowl;
+    const int pix = k / 64, ch = k % 64;
+    const int py = pix / 6, px = pix % 6;
+    const int dzoff = ((2 * py + (c32 >> 1)) * 13 + 2 * px + (c32 & 1)) * 64 + ch;
+    fvec4 g[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] = z4;
+    for (int c0 = 0; c0 < count; c0 += D5_SCHUNK) {
+      const int cn = min(D5_SCHUNK, count - c0);
+      if (!one_chunk) {
+        __syncthreads();
+        stage(c0, cn);
+        __syncthreads();
+      }
+      for (int jj = 0; jj < cn; ++jj) {
+        const float pv = p_s[jj * KB + grp * D5_ROWS + rowl];
+        float d = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const fvec4 dh = dh_s[jj * (HID / 4) + c32 + 32 * i];
+          g[i].x += pv * dh.x; g[i].y += pv * dh.y; g[i].z += pv * dh.z; g[i].w += pv * dh.w;
+          d += dh.x * w[i].x; d += dh.y * w[i].y; d += dh.z * w[i].z; d += dh.w * w[i].w;
+        }
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        d += __shfl_xor(d, 8, 64);
+        d += __shfl_xor(d, 16, 64);
+        if (c32 < 4) {  // un-pool: lane c32 = q writes window pixel q
+          const uint32_t c = c_s[jj * KB + grp * D5_ROWS + rowl];
+          const float v = (c & CODE_KEEP) ? d * SCALE_25 : 0.0f;
+          const bool hit = (c & CODE_POS) && (int)(c & 3) == c32;
+          dZ4[((int64_t)r * bmax + c0 + jj) * MPLC_CIFAR_DZ4 + dzoff] = hit ? v : 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fvec4 pw = w[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float p1 = pw[q], a1 = av[i][q];
+        rms_apply(p1, a1, g[i][q], cfg);
+        pw[q] = p1;
+        av[i][q] = a1;
+      }
+      W[32 * i] = pw;
+      __builtin_nontemporal_store(av[i], Ra + 32 * i);
+    }
+    W = Wn;
+    Ra = Ran;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[i] = wn[i];
+      av[i] = avn[i];
+    }
   }
   if (blockIdx.x == 0) {
     const float* dHs = dH + (int64_t)r * bmax * HID;
@@ -861,12 +963,12 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 // BR, NW> (wgrad); geometry checked by static_asserts, LDS per block in the comment
 // ------------------------------------------------------------------------------------------------
 #define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
-#define CONV2_FWD conv_kernel<32, 32, 32, 32, 0, 5, 5, 2, EPI_FWD_POOL>    /* 3 bands, 50.7 KB */
-#define CONV3_FWD conv_kernel<15, 15, 32, 64, 1, 15, 4, 2, EPI_FWD>        /* 1 band,  38.1 KB */
-#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 5, 1, EPI_FWD_POOL>    /* 1 band,  54.6 KB */
-#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 8, 4, 1, EPI_BWD_MASK>  /* 2 bands, 44.2 KB */
-#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 8, 4, 1, EPI_BWD_UNPOOL>/* 2 bands, 44.2 KB */
-#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 8, 4, 2, EPI_BWD_MASK>  /* 4 bands, 44.9 KB */
+#define CONV2_FWD conv_kernel<32, 32, 32, 32, 0, 4, 4, 2, EPI_FWD_POOL>    /* 4 bands, 42.6 KB */
+#define CONV3_FWD conv_kernel<15, 15, 32, 64, 1, 16, 4, 2, EPI_FWD>        /* 1 band,  42.0 KB */
+#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 3, 2, EPI_FWD_POOL>    /* 1 band,  56.0 KB */
+#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 8, 4, 1, EPI_BWD_MASK>  /* 2 bands, 45.1 KB */
+#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 8, 4, 1, EPI_BWD_UNPOOL>/* 2 bands, 45.1 KB */
+#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 8, 4, 2, EPI_BWD_MASK>  /* 4 bands, 45.1 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 #define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 5, 3>
 #define CONV3_WGRAD wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 5, 3>
@@ -916,7 +1018,7 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   c2.out = d2;
   c2.code_out = code2;
   PB(2);
-  CONV2_FWD<<<dim3(3, B, R), 320, 0, s>>>(c2);
+  CONV2_FWD<<<dim3(4, B, R), 256, 0, s>>>(c2);
   PE(2);
   ConvArgs c3 = conv_args(d2, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W3, stride);
   c3.bias = params + OFF_B3;
@@ -933,7 +1035,7 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   c4.out = d4;
   c4.code_out = code4;
   PB(4);
-  CONV4_FWD<<<dim3(1, B, R), 320, 0, s>>>(c4);
+  CONV4_FWD<<<dim3(1, B, R), 192, 0, s>>>(c4);
   PE(4);
   PB(5);
   dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, drop_key,
@@ -981,7 +1083,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                                 t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
   PROF_END(6);
   PROF_BEGIN(7);
-  dense5_bwd_kernel<<<dim3(FEAT / D5_ROWS, R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
+  dense5_bwd_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
                                                             t->rms, t->dz4, t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
   PROF_END(7);
   transpose_w_kernel<<<dim3(32, R), 256, 0, s>>>(t->params, t->cnt, t->wt);

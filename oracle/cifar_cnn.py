@@ -53,14 +53,28 @@ def single_drop_key(key, e, t):
     return ocnn.subkey(key, 0x50000 + e, t)
 
 
+def hash32(x):
+    """lowbias32 finaliser on uint32 arrays (csrc/cifar_cnn.hip hash32)."""
+    x = np.asarray(x, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7feb352d)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846ca68b)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
 def dropout_keep(dkey, layer, count, n):
-    """[count, n] bool keep mask of one layer at one step (slot j = row, element e = NHWC flat index)."""
+    """[count, n] bool keep mask of one layer at one step (slot j = row, element e = NHWC flat index):
+    hash32(row_seed(j) ^ e) >> 8 >= rate * 2^24, row_seed = hash32(lo(key) ^ hash32(hi(key) ^ layer<<24 ^ j))."""
     lid, thr = DROP[layer]
-    j = np.arange(count, dtype=np.uint64)[:, None]
-    e = np.arange(n, dtype=np.uint64)[None, :]
-    word = (np.uint64(lid) << np.uint64(56)) | (j << np.uint64(32)) | e
-    h = ocnn.mix64_np(np.uint64(dkey) ^ ocnn.mix64_np(word))
-    return (h >> np.uint64(40)) >= np.uint64(thr)
+    dkey = int(dkey)
+    j = np.arange(count, dtype=np.uint32)
+    inner = hash32(np.uint32(dkey >> 32) ^ np.uint32(lid << 24) ^ j)
+    seed = hash32(np.uint32(dkey & 0xFFFFFFFF) ^ inner)[:, None]
+    e = np.arange(n, dtype=np.uint32)[None, :]
+    return (hash32(seed ^ e) >> np.uint32(8)) >= np.uint32(thr)
 
 
 def step_masks(dkey, count):

@@ -117,7 +117,9 @@ def test_cifar_sequential_accuracies_vs_oracle(approach):
     bs = [p.batch_size for p in sc.partners_list]
     ds = sc.dataset
     data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    coals = [(0, 1), (0, 1, 2)]
+    # 297 test samples (1 sample = 0.34 pt) and fp32 summation-order differences amplified over 2 epochs of
+    # training: the +-1 pt bar is on the mean over several coalitions
+    coals = [(0, 1), (0, 2), (1, 2), (0, 1, 2)]
     dev = eng.evaluate(coals)
     ref = np.array([occ.coalition_value(data, prow, bs, c, seed=eng.seed, epochs=eng.epoch_count,
                                         M=eng.minibatch_count, approach=approach)[0] for c in coals])
