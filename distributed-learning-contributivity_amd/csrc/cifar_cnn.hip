@@ -217,8 +217,10 @@ __host__ __device__ constexpr int ci3_off(int k, int rowp) { return (k / 9) * ro
 // of pool windows with lane m = window * 4 + q (so the 4 pixels of a window are accumulator registers
 // 4g..4g+3 of one lane: the pool is a register max).  With the LDS row stride = 8 (mod 32) dwords and an
 // odd pixel stride, the 32 pixels of a tile fall on 32 distinct banks.
-template <int HI, int WI, int CI, int CO, int PAD, int BR, int NW, int UM, int EPI>
+template <int HI, int WI, int CI, int CO, int PAD, int BR, int NW, int UM, int EPI, int CS = 1>
 __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
+  // CS channel slices: the input band is staged CI / CS channels at a time (K split), so a band (or a whole
+  // sample) with many tiles per wave fits a small LDS footprint
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
   constexpr int PH = HO / 2, PW = WO / 2;
@@ -226,13 +228,15 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
   constexpr int TX = POOL ? (PW + 3) / 4 : (WO + 7) / 8;
   constexpr int TY = POOL ? BR / 2 : BR / 4;
   constexpr int TILES = TX * TY;
-  constexpr int LR = ROWS + 2, WIP = WI + 2 * PAD, CIP = CI | 1;
+  constexpr int CIS = CI / CS;  // channels per slice
+  constexpr int LR = ROWS + 2, WIP = WI + 2 * PAD, CIP = CIS | 1;
   constexpr int ROWP = WIP * CIP + ((8 - (WIP * CIP) % 32) + 32) % 32;
   constexpr int NT = CO / 32;
   constexpr int NTHR = NW * 64;
   static_assert(POOL ? BR % 2 == 0 : BR % 4 == 0, "bands are whole tile rows");
   static_assert(NW * UM >= TILES, "row tiles do not cover the band");
-  static_assert(CO % 32 == 0 && (CI == 3 || CI % 4 == 0), "unsupported channel counts");
+  static_assert(CO % 32 == 0 && (CI == 3 || CIS % 4 == 0) && CI % CS == 0, "unsupported channel counts");
+  static_assert(CI != 3 || CS == 1, "the 3-channel input is not sliced");
   __shared__ float in_s[LR * ROWP];
   const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
@@ -244,39 +248,42 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
                      : a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ
                                       : a.in + slot * IN_SZ;
   const int y0 = band * ROWS;
-  if constexpr (CI % 4 == 0) {
-    // 16-B loads along the channels; each thread keeps one channel quad and walks pixels incrementally
-    constexpr int C4 = CI / 4;
-    static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
-    constexpr int PSTEP = NTHR / C4;
-    const int c4 = tid % C4;
-    int pix = tid / C4;
-    int rr = pix / WIP, col = pix % WIP;
-    for (; pix < LR * WIP; pix += PSTEP) {
-      const int iy = y0 - PAD + rr, ix = col - PAD;
-      fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
-        v = *reinterpret_cast<const fvec4*>(src + (iy * WI + ix) * CI + 4 * c4);
-      float* d = in_s + rr * ROWP + col * CIP + 4 * c4;
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-      col += PSTEP % WIP;
-      rr += PSTEP / WIP;
-      if (col >= WIP) { col -= WIP; ++rr; }
+  // stage channels [cs * CIS, (cs + 1) * CIS) of the band's input rows
+  auto stage = [&](int cs) {
+    if constexpr (CI % 4 == 0) {
+      // 16-B loads along the channels; each thread keeps one channel quad and walks pixels incrementally
+      constexpr int C4 = CIS / 4;
+      static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
+      constexpr int PSTEP = NTHR / C4;
+      const int c4 = tid % C4;
+      int pix = tid / C4;
+      int rr = pix / WIP, col = pix % WIP;
+      for (; pix < LR * WIP; pix += PSTEP) {
+        const int iy = y0 - PAD + rr, ix = col - PAD;
+        fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
+          v = *reinterpret_cast<const fvec4*>(src + (iy * WI + ix) * CI + cs * CIS + 4 * c4);
+        float* d = in_s + rr * ROWP + col * CIP + 4 * c4;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+        col += PSTEP % WIP;
+        rr += PSTEP / WIP;
+        if (col >= WIP) { col -= WIP; ++rr; }
+      }
+    } else {
+      for (int e = tid; e < LR * WIP * CI; e += NTHR) {
+        const int c = e % CI;
+        const int col = (e / CI) % WIP;
+        const int rr = e / (CI * WIP);
+        const int iy = y0 - PAD + rr, ix = col - PAD;
+        float v = 0.0f;
+        if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
+        in_s[rr * ROWP + col * CIP + c] = v;
+      }
     }
-  } else {
-    for (int e = tid; e < LR * WIP * CI; e += NTHR) {
-      const int c = e % CI;
-      const int col = (e / CI) % WIP;
-      const int rr = e / (CI * WIP);
-      const int iy = y0 - PAD + rr, ix = col - PAD;
-      float v = 0.0f;
-      if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
-      in_s[rr * ROWP + col * CIP + c] = v;
-    }
-  }
+  };
   const int lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31, kh = lane >> 5;
   int abase[UM];
@@ -306,8 +313,9 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[u][nt] = zero16();
   const float* W = a.w + (int64_t)r * a.w_rstride;
-  __syncthreads();
   if constexpr (CI == 3) {
+    stage(0);
+    __syncthreads();
     // K = 27 taps x channels, padded to 28: lane half kh takes k = 2s + kh
     const float* Wl = W + kh * CO + n;
 #pragma unroll
@@ -322,20 +330,25 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
       }
     }
   } else {
+    for (int cs = 0; cs < CS; ++cs) {
+      if (cs) __syncthreads();  // the previous slice's readers are done
+      stage(cs);
+      __syncthreads();
 #pragma unroll
-    for (int kyx = 0; kyx < 9; ++kyx) {
-      const int offA = (kyx / 3) * ROWP + (kyx % 3) * CIP;
-      const float* Wk = W + (int64_t)(kyx * CI + kh) * CO + n;
+      for (int kyx = 0; kyx < 9; ++kyx) {
+        const int offA = (kyx / 3) * ROWP + (kyx % 3) * CIP;
+        const float* Wk = W + (int64_t)(kyx * CI + cs * CIS + kh) * CO + n;
 #pragma unroll
-      for (int c2 = 0; c2 < CI / 2; ++c2) {
-        float b[NT];
+        for (int c2 = 0; c2 < CIS / 2; ++c2) {
+          float b[NT];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b[nt] = Wk[2 * c2 * CO + nt * 32];
+          for (int nt = 0; nt < NT; ++nt) b[nt] = Wk[2 * c2 * CO + nt * 32];
 #pragma unroll
-        for (int u = 0; u < UM; ++u) {
-          const float av = in_s[abase[u] + offA + 2 * c2];
+          for (int u = 0; u < UM; ++u) {
+            const float av = in_s[abase[u] + offA + 2 * c2];
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[u][nt] = mfma32(av, b[nt], acc[u][nt]);
+            for (int nt = 0; nt < NT; ++nt) acc[u][nt] = mfma32(av, b[nt], acc[u][nt]);
+          }
         }
       }
     }
@@ -965,10 +978,10 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
 #define CONV2_FWD conv_kernel<32, 32, 32, 32, 0, 4, 4, 2, EPI_FWD_POOL>    /* 4 bands, 42.6 KB */
 #define CONV3_FWD conv_kernel<15, 15, 32, 64, 1, 16, 4, 2, EPI_FWD>        /* 1 band,  42.0 KB */
-#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 3, 2, EPI_FWD_POOL>    /* 1 band,  56.0 KB */
-#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 8, 4, 1, EPI_BWD_MASK>  /* 2 bands, 45.1 KB */
-#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 8, 4, 1, EPI_BWD_UNPOOL>/* 2 bands, 45.1 KB */
-#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 8, 4, 2, EPI_BWD_MASK>  /* 4 bands, 45.1 KB */
+#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 3, 2, EPI_FWD_POOL, 2>  /* 1 band,  29.1 KB */
+#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 16, 4, 2, EPI_BWD_MASK, 2> /* 1 band, 42.0 KB */
+#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 16, 4, 2, EPI_BWD_UNPOOL, 2> /* 1 band, 42.0 KB */
+#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 16, 4, 4, EPI_BWD_MASK, 2> /* 2 bands, 42.0 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 #define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 5, 3>
 #define CONV3_WGRAD wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 5, 3>
@@ -1096,7 +1109,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   g4.aux = t->a3;
   g4.out = t->dz3;
   PROF_BEGIN(9);
-  CONV4_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g4);
+  CONV4_DGRAD<<<dim3(1, B, R), 256, 0, s>>>(g4);
   PROF_END(9);
   WgArgs w3{t->d2, 0, t->idx, t->cnt, B, SP, t->dz3, t->wpart, (int)OFF_W3, (int)OFF_B3};
   PROF_BEGIN(10);
@@ -1106,7 +1119,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   g3.code_in = t->code2;
   g3.out = t->dz2;
   PROF_BEGIN(11);
-  CONV3_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g3);
+  CONV3_DGRAD<<<dim3(1, B, R), 256, 0, s>>>(g3);
   PROF_END(11);
   WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2};
   PROF_BEGIN(12);
@@ -1116,7 +1129,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   g2.aux = t->a1;
   g2.out = t->dz1;
   PROF_BEGIN(13);
-  CONV2_DGRAD<<<dim3(4, B, R), 256, 0, s>>>(g2);
+  CONV2_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g2);
   PROF_END(13);
   WgArgs w1{t->x, 1, t->idx, t->cnt, B, SP, t->dz1, t->wpart, (int)OFF_W1, (int)OFF_B1};
   PROF_BEGIN(14);
