@@ -1,4 +1,5 @@
-"""Summarise PMC passes (rocprofv3 --pmc, one directory per pass) per kernel: VALU/MFMA instruction ratio,
+"""Summarise PMC passes (rocprofv3 --pmc, one directory per pass) per kernel: MFMA-pipe busy fraction,
+VALU/MFMA instruction ratio,
 LDS bank-conflict share, wait share, VMEM reads per MFMA, FETCH bytes (x2 gfx950 correction).
 python scripts/pmc_summary.py <dir with p1 p2 p3 ...>"""
 import collections
@@ -11,9 +12,12 @@ for f in glob.glob(f"{sys.argv[1]}/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
-print(f"{'kernel':44s} {'valu/mfma':>9s} {'lds_conf':>8s} {'wait/act':>8s} {'vmem/mfma':>9s} {'fetch GB':>9s}")
+print(f"{'kernel':44s} {'mfma_busy':>9s} {'valu/mfma':>9s} {'lds_conf':>8s} {'wait/act':>8s} {'vmem/mfma':>9s} {'fetch GB':>9s}")
 for k, v in tot.items():
     mf = v["SQ_INSTS_MFMA"] + 1e-9
-    print(f"{k[:44]:44s} {v['SQ_INSTS_VALU'] / mf:9.2f} {v['SQ_LDS_BANK_CONFLICT'] / (v['SQ_LDS_IDX_ACTIVE'] + 1):8.3f} "
+    # MFMA pipe utilisation: busy cycles over all 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE sums the
+    # 8 XCDs, MI355X_MICROARCH.md)
+    busy = v["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, v["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    print(f"{k[:44]:44s} {busy:9.3f} {v['SQ_INSTS_VALU'] / mf:9.2f} {v['SQ_LDS_BANK_CONFLICT'] / (v['SQ_LDS_IDX_ACTIVE'] + 1):8.3f} "
           f"{v['SQ_WAIT_INST_ANY'] / (v['SQ_ACTIVE_INST_ANY'] + 1):8.2f} {v['SQ_INSTS_VMEM_RD'] / mf:9.2f} "
           f"{2 * v['FETCH_SIZE'] / 1024 / 1024:9.2f}")
