@@ -34,6 +34,8 @@ for _p in (REPO, PKG):
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (v_mfma_f32_32x32x2_f32), spec
 CONV_BWD_DATA_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2  # dA1 = dZ2 (*) W2 over all conv1 positions
+MNIST_FWD_FLOP = 23984896       # per sample, SURVEY A21
+MNIST_TRAIN_FLOP = 71565312     # per sample (fwd + wgrad + dgrad, no conv1 dgrad)
 
 
 def pmc_traffic(kernel, workload):
@@ -287,6 +289,11 @@ def bench_train(args, rank, world):
                      "flop_per_sample": CONV_BWD_DATA_FLOP_PER_SAMPLE},
         "shapley_values": [round(float(v), 6) for v in c.contributivity_scores],
     }
+    # whole-job algorithmic rate: training 2*E*sum n_p samples x 71.57 MFLOP + test evaluation
+    # 1023 x 10000 x 23.98 MFLOP (MNIST CNN forward / train FLOPs per sample)
+    job_flop = total_train_samples / args.steps * MNIST_TRAIN_FLOP + n_coal * len(sc.dataset.x_test) * MNIST_FWD_FLOP
+    out["algorithmic"] = {"flop_per_step": int(job_flop), "tflops": round(job_flop / (ms_per_step / 1000) / 1e12, 2),
+                          "frac_of_fp32_mfma_peak": round(job_flop / (ms_per_step / 1000) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
     return out, sc
 
 
@@ -398,7 +405,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
-    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar"])
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
