@@ -251,36 +251,54 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
   // stage channels [cs * CIS, (cs + 1) * CIS) of the band's input rows
   auto stage = [&](int cs) {
     if constexpr (CI % 4 == 0) {
-      // 16-B loads along the channels; each thread keeps one channel quad and walks pixels incrementally
+      // 16-B loads along the channels, all issued before the first LDS store (an exposed load -> wait ->
+      // store chain per element would serialise the memory latency); out-of-image pixels load a valid
+      // address and are zeroed by a select
       constexpr int C4 = CIS / 4;
-      static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
-      constexpr int PSTEP = NTHR / C4;
-      const int c4 = tid % C4;
-      int pix = tid / C4;
-      int rr = pix / WIP, col = pix % WIP;
-      for (; pix < LR * WIP; pix += PSTEP) {
-        const int iy = y0 - PAD + rr, ix = col - PAD;
-        fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
-          v = *reinterpret_cast<const fvec4*>(src + (iy * WI + ix) * CI + cs * CIS + 4 * c4);
-        float* d = in_s + rr * ROWP + col * CIP + 4 * c4;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
-        col += PSTEP % WIP;
-        rr += PSTEP / WIP;
-        if (col >= WIP) { col -= WIP; ++rr; }
+      constexpr int TOT = LR * WIP * C4;
+      constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+      fvec4 v[NIT];
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int e4 = tid + k * NTHR;
+        const int pix = e4 / C4, c4 = e4 % C4;
+        const int iy = y0 - PAD + pix / WIP, ix = pix % WIP - PAD;
+        const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+        const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? src + (iy * WI + ix) * CI + cs * CIS + 4 * c4 : src);
+        v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int e4 = tid + k * NTHR;
+        if (e4 < TOT) {
+          const int pix = e4 / C4, c4 = e4 % C4;
+          float* d = in_s + (pix / WIP) * ROWP + (pix % WIP) * CIP + 4 * c4;
+          d[0] = v[k].x;
+          d[1] = v[k].y;
+          d[2] = v[k].z;
+          d[3] = v[k].w;
+        }
       }
     } else {
-      for (int e = tid; e < LR * WIP * CI; e += NTHR) {
-        const int c = e % CI;
-        const int col = (e / CI) % WIP;
-        const int rr = e / (CI * WIP);
-        const int iy = y0 - PAD + rr, ix = col - PAD;
-        float v = 0.0f;
-        if (iy >= 0 && iy < HI && ix >= 0 && ix < WI) v = src[(iy * WI + ix) * CI + c];
-        in_s[rr * ROWP + col * CIP + c] = v;
+      constexpr int TOT = LR * WIP * CI;
+      constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+      float v[NIT];
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int e = tid + k * NTHR;
+        const int c = e % CI, pix = e / CI;
+        const int iy = y0 - PAD + pix / WIP, ix = pix % WIP - PAD;
+        const bool ok = e < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+        const float t = *(ok ? src + (iy * WI + ix) * CI + c : src);
+        v[k] = ok ? t : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int e = tid + k * NTHR;
+        if (e < TOT) {
+          const int c = e % CI, pix = e / CI;
+          in_s[(pix / WIP) * ROWP + (pix % WIP) * CIP + c] = v[k];
+        }
       }
     }
   };
@@ -512,44 +530,65 @@ __global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
     for (int band = 0; band < NB; ++band) {
       const int y0 = band * BR;
       __syncthreads();  // previous band's readers done
-      if constexpr (CI % 4 == 0) {  // 16-B loads and ds_write_b128, incremental pixel walk
-        constexpr int C4 = CI / 4, PSTEP = NTHR / C4;
-        static_assert(NTHR % C4 == 0, "fixed channel quad per thread");
-        const int c4 = tid % C4;
-        int pix = tid / C4;
-        int rr = pix / WXP, col = pix % WXP;
-        for (; pix < (BR + 2) * WXP; pix += PSTEP) {
-          const int iy = y0 - PAD + rr, ix = col - PAD;
-          fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-          if (iy >= 0 && iy < HI && ix >= 0 && ix < WI)
-            v = *reinterpret_cast<const fvec4*>(X + (iy * WI + ix) * CI + 4 * c4);
-          *reinterpret_cast<fvec4*>(x_s + pix * CI + 4 * c4) = v;
-          col += PSTEP % WXP;
-          rr += PSTEP / WXP;
-          if (col >= WXP) { col -= WXP; ++rr; }
+      if constexpr (CI % 4 == 0) {  // 16-B loads, all in flight before the ds_write_b128 stores
+        constexpr int C4 = CI / 4;
+        constexpr int TOT = (BR + 2) * WXP * C4;
+        constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+        fvec4 v[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * NTHR;
+          const int pix = e4 / C4, c4 = e4 % C4;
+          const int iy = y0 - PAD + pix / WXP, ix = pix % WXP - PAD;
+          const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? X + (iy * WI + ix) * CI + 4 * c4 : X);
+          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * NTHR;
+          if (e4 < TOT) *reinterpret_cast<fvec4*>(x_s + 4 * e4) = v[k];
         }
       } else {
-        for (int e = tid; e < (BR + 2) * WXP * CI; e += NTHR) {
-          const int c = e % CI;
-          const int col = (e / CI) % WXP;
-          const int rr = e / (CI * WXP);
-          const int iy = y0 - PAD + rr, ix = col - PAD;
-          x_s[e] = (iy >= 0 && iy < HI && ix >= 0 && ix < WI) ? X[(iy * WI + ix) * CI + c] : 0.0f;
+        constexpr int TOT = (BR + 2) * WXP * CI;
+        constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+        float v[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e = tid + k * NTHR;
+          const int c = e % CI, pix = e / CI;
+          const int iy = y0 - PAD + pix / WXP, ix = pix % WXP - PAD;
+          const bool ok = e < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+          const float t = *(ok ? X + (iy * WI + ix) * CI + c : X);
+          v[k] = ok ? t : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e = tid + k * NTHR;
+          if (e < TOT) x_s[e] = v[k];
         }
       }
       {
-        constexpr int Z4 = CO / 4, PSTEP = NTHR / Z4;  // each thread: one channel quad of dZ (db too)
-        int pix = tid / Z4;
-        int yy = pix / WOE, xx = pix % WOE;
-        for (; pix < BR * WOE; pix += PSTEP) {
-          fvec4 v = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-          if (y0 + yy < HOV && xx < WOV)
-            v = *reinterpret_cast<const fvec4*>(Z + ((y0 + yy) * WO + xx) * CO + 4 * (tid % Z4));
-          *reinterpret_cast<fvec4*>(z_s + pix * CO + 4 * (tid % Z4)) = v;
-          gb += v;
-          xx += PSTEP % WOE;
-          yy += PSTEP / WOE;
-          if (xx >= WOE) { xx -= WOE; ++yy; }
+        constexpr int Z4 = CO / 4;  // each thread: one channel quad of dZ (db too)
+        constexpr int TOT = BR * WOE * Z4;
+        constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+        fvec4 v[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * NTHR;
+          const int pix = e4 / Z4, c4 = e4 % Z4;
+          const int yy = y0 + pix / WOE, xx = pix % WOE;
+          const bool ok = e4 < TOT && yy < HOV && xx < WOV;
+          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? Z + (yy * WO + xx) * CO + 4 * c4 : Z);
+          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * NTHR;
+          if (e4 < TOT) {
+            *reinterpret_cast<fvec4*>(z_s + 4 * e4) = v[k];
+            gb += v[k];  // channel quad e4 % (CO/4) == tid % (CO/4): NTHR is a multiple of CO/4
+          }
         }
       }
       __syncthreads();
@@ -650,20 +689,38 @@ __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict
   const float* Ar = A + (int64_t)r * bmax * FEAT;
   const float* W = params + (int64_t)r * stride + OFF_W5;
   floatx16 acc = zero16();
-  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
-    for (int e = tid; e < 32 * DF_K; e += 256) {
+  // software pipeline over K chunks: the next chunk's A tile (8 values per thread) and W5 column slice
+  // (32 values per lane) load into registers while this chunk's 32 MFMAs run
+  constexpr int AIT = 32 * DF_K / 256;
+  const float* wl = W + n0 + (lane & 31) + (int64_t)kh * HID;
+  float av[AIT], bv[DF_K / 2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
       const int mm = e / DF_K, kk = e % DF_K;
-      a_s[mm * (DF_K + 1) + kk] = (m0 + mm < count) ? Ar[(int64_t)(m0 + mm) * FEAT + k0 + kk] : 0.0f;
+      const bool ok = m0 + mm < count;
+      const float t = Ar[(int64_t)(ok ? m0 + mm : m0) * FEAT + k0 + kk];
+      av[i] = ok ? t : 0.0f;
     }
-    __syncthreads();
-    const float* Wk = W + (int64_t)k0 * HID + n0 + (lane & 31);
-#pragma unroll 8
-    for (int s = 0; s < DF_K / 2; ++s) {
-      const float av = a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh];
-      const float b = Wk[(int64_t)(2 * s + kh) * HID];
-      acc = mfma32(av, b, acc);
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) bv[s] = wl[(int64_t)(k0 + 2 * s) * HID];
+  };
+  load(0);
+  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
+    __syncthreads();  // previous chunk's readers done
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
+      a_s[(e / DF_K) * (DF_K + 1) + e % DF_K] = av[i];
     }
+    float bc[DF_K / 2];
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) bc[s] = bv[s];
+    load(min(k0 + DF_K, FEAT - DF_K));  // the last chunk re-loads itself (uniform, branch-free)
     __syncthreads();
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) acc = mfma32(a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh], bc[s], acc);
   }
   const int col = n0 + (lane & 31);
   const float bias = params[(int64_t)r * stride + OFF_B5 + col];

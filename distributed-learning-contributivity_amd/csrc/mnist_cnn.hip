@@ -159,7 +159,18 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   const int row = idx ? idx[(int64_t)r * bmax + j] : row_base + j;
   const float* P = params + (int64_t)r * stride;
   const float* xi = x + (int64_t)row * (IMG * IMG) + half * 12 * IMG;
-  for (int e = tid; e < 16 * IMG; e += FWD_THREADS) img_s[e] = xi[e];
+  {  // all of the block's image loads in flight at once
+    constexpr int NIT = (16 * IMG + FWD_THREADS - 1) / FWD_THREADS;
+    float v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + FWD_THREADS * k;
+      v[k] = xi[e < 16 * IMG ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k)
+      if (tid + FWD_THREADS * k < 16 * IMG) img_s[tid + FWD_THREADS * k] = v[k];
+  }
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int m = lane & 31;
@@ -263,21 +274,39 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict_
   const float* Ar = A + (int64_t)r * a_rstride;
   const float* W = params + (int64_t)r * stride + OFF_W3;
   floatx16 acc = zero16();
-  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
-    // stage A[m0..m0+31][k0..k0+63] (rows beyond count are zero)
-    for (int e = tid; e < 32 * DF_K; e += 256) {
+  // software pipeline over K chunks: the next chunk's A tile (8 values per thread) and W3 column slice
+  // (32 values per lane) are loaded into registers while this chunk's 32 MFMAs run, so neither the LDS
+  // staging nor the MFMA chain ever waits on a single exposed load
+  constexpr int AIT = 32 * DF_K / 256;
+  const float* wl = W + n0 + (lane & 31) + (int64_t)kh * HID;
+  float av[AIT], bv[DF_K / 2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
       const int mm = e / DF_K, kk = e % DF_K;
-      a_s[mm * (DF_K + 1) + kk] = (m0 + mm < count) ? Ar[(int64_t)(m0 + mm) * FEAT + k0 + kk] : 0.0f;
+      const bool ok = m0 + mm < count;
+      const float t = Ar[(int64_t)(ok ? m0 + mm : m0) * FEAT + k0 + kk];
+      av[i] = ok ? t : 0.0f;
     }
-    __syncthreads();
-    const float* Wk = W + (int64_t)k0 * HID + n0 + (lane & 31);
-#pragma unroll 8
-    for (int s = 0; s < DF_K / 2; ++s) {
-      const float a = a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh];
-      const float b = Wk[(int64_t)(2 * s + kh) * HID];
-      acc = mfma32(a, b, acc);
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) bv[s] = wl[(int64_t)(k0 + 2 * s) * HID];
+  };
+  load(0);
+  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
+    __syncthreads();  // previous chunk's readers done
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
+      a_s[(e / DF_K) * (DF_K + 1) + e % DF_K] = av[i];
     }
+    float bc[DF_K / 2];
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) bc[s] = bv[s];
+    load(min(k0 + DF_K, FEAT - DF_K));  // the last chunk re-loads itself (uniform, branch-free)
     __syncthreads();
+#pragma unroll
+    for (int s = 0; s < DF_K / 2; ++s) acc = mfma32(a_s[(lane & 31) * (DF_K + 1) + 2 * s + kh], bc[s], acc);
   }
   const float bias = params[(int64_t)r * stride + OFF_B3 + n0 + (lane & 31)];
 #pragma unroll
@@ -457,10 +486,27 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   float* dPr = dPool + (int64_t)r * bmax * FEAT;
   for (int c0 = 0; c0 < count; c0 += D1_SCHUNK) {
     const int cn = min(D1_SCHUNK, count - c0);
-    for (int e = tid; e < cn * (HID / 4); e += 256) dh_s[e] = dHr[(int64_t)c0 * (HID / 4) + e];
-    for (int e = tid; e < cn * D1_ROWS; e += 256) {
-      const int jj = e / D1_ROWS, kk = e % D1_ROWS;
-      p_s[e] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + kk];
+    {  // every staging load in flight before the first LDS store (clamped index, no branch on the load)
+      constexpr int HIT = D1_SCHUNK * (HID / 4) / 256, PIT = D1_SCHUNK * D1_ROWS / 256;
+      fvec4 hv[HIT];
+      float pv[PIT];
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int e = tid + 256 * i;
+        hv[i] = dHr[(int64_t)c0 * (HID / 4) + (e < cn * (HID / 4) ? e : 0)];
+      }
+#pragma unroll
+      for (int i = 0; i < PIT; ++i) {
+        const int e = tid + 256 * i;
+        const int jj = e < cn * D1_ROWS ? e / D1_ROWS : 0;
+        pv[i] = Pr[(int64_t)(c0 + jj) * FEAT + k0 + e % D1_ROWS];
+      }
+#pragma unroll
+      for (int i = 0; i < HIT; ++i)
+        if (tid + 256 * i < cn * (HID / 4)) dh_s[tid + 256 * i] = hv[i];
+#pragma unroll
+      for (int i = 0; i < PIT; ++i)
+        if (tid + 256 * i < cn * D1_ROWS) p_s[tid + 256 * i] = pv[i];
     }
     __syncthreads();
 #pragma unroll 2
@@ -578,7 +624,19 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   const int oy0 = iy0 - 2;             // dZ2 row of local row 0
   const int pr0 = (oy0 + 2) / 2 - 1;  // first pooled row touching the band (-1 or 5)
   for (int e = tid; e < DZR * DZC * DZQ; e += BWD_THREADS) dz_s[e] = 0.0f;
-  for (int e = tid; e < (BAND + 2) * IMG; e += BWD_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + iy0 * IMG + e];
+  {
+    constexpr int NIT = ((BAND + 2) * IMG + BWD_THREADS - 1) / BWD_THREADS;
+    const float* xr = x + (int64_t)row * IMG * IMG + iy0 * IMG;
+    float v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + BWD_THREADS * k;
+      v[k] = xr[e < (BAND + 2) * IMG ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k)
+      if (tid + BWD_THREADS * k < (BAND + 2) * IMG) img_s[tid + BWD_THREADS * k] = v[k];
+  }
   const int lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31;
   const int kh = lane >> 5;
@@ -717,15 +775,28 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       pcd[s] = code[base + e];
     }
   };
+  // the sample's image is fetched into registers one sample ahead (with its dataset row index)
+  constexpr int IMG_PRE = (IMG * IMG + WG_THREADS - 1) / WG_THREADS;
+  float imgv[IMG_PRE];
+  auto fetch_img = [&](int jj) {
+    const float* xr = x + (int64_t)idx[(int64_t)r * bmax + jj] * (IMG * IMG);
+#pragma unroll
+    for (int k = 0; k < IMG_PRE; ++k) {
+      const int e = tid + WG_THREADS * k;
+      imgv[k] = xr[e < IMG * IMG ? e : 0];
+    }
+  };
   fetch(j_begin, 0);
+  fetch_img(j_begin);
   // A-operand bases: row tile u = (ky = wave, kx = u) x 32 ci, lane (kh, m) reads pixel px0 + kh, channel m
   const int zb = kh * WGP + m;
   int ab[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) ab[u] = (wave * A1 + u) * C1 + kh * C1 + m;
   for (int j = j_begin; j < j_end; ++j) {
-    const int row = idx[(int64_t)r * bmax + j];
-    for (int e = tid; e < IMG * IMG; e += WG_THREADS) img_s[e] = x[(int64_t)row * IMG * IMG + e];
+#pragma unroll
+    for (int k = 0; k < IMG_PRE; ++k)
+      if (tid + WG_THREADS * k < IMG * IMG) img_s[tid + WG_THREADS * k] = imgv[k];
     for (int band = 0; band < 6; ++band) {
       __syncthreads();  // img_s loaded; previous band's MFMA readers done
 #pragma unroll
@@ -756,8 +827,12 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
           }
         }
       }
-      if (band < 5) fetch(j, band + 1);
-      else if (j + 1 < j_end) fetch(j + 1, 0);
+      if (band < 5) {
+        fetch(j, band + 1);
+      } else if (j + 1 < j_end) {
+        fetch(j + 1, 0);
+        fetch_img(j + 1);
+      }
       __syncthreads();
       // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh): px = 2*s2 + kh
 #pragma unroll
