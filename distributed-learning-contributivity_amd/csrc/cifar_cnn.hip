@@ -756,13 +756,17 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
                                                    const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t,
                                                    int bmax, float* __restrict__ params, float* __restrict__ rms,
                                                    float* __restrict__ dH, float lr, float rho, float omr,
-                                                   float decay, float eps) {
+                                                   float decay, float eps, double* __restrict__ hstats) {
   __shared__ float w6_s[W6N];
   __shared__ float dl_s[HEAD_CHUNK * NCLS];
+  __shared__ double hs_s[2][HEAD_CHUNK];
   const int r = blockIdx.x;
   const int count = cnt[r];
-  if (count == 0) return;
   const int tid = threadIdx.x;
+  if (count == 0) {
+    if (hstats && tid < 3) hstats[(int64_t)r * 3 + tid] = 0.0;
+    return;
+  }
   float* P = params + (int64_t)r * STRIDE;
   for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
   __syncthreads();
@@ -770,6 +774,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
   float gacc[HEAD_G];
 #pragma unroll
   for (int u = 0; u < HEAD_G; ++u) gacc[u] = 0.0f;
+  double hl = 0.0, hc = 0.0;  // this thread's training CE / correct sums (hstats)
   const float* Dr = D5 + (int64_t)r * bmax * HID;
   for (int c0 = 0; c0 < count; c0 += HEAD_CHUNK) {
     const int cn = min(HEAD_CHUNK, count - c0);
@@ -784,13 +789,20 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 #pragma unroll
         for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
       }
+      const int y = labels[idx[(int64_t)r * bmax + jj]];
+      int am = 0;  // first maximum (the evaluation's argmax)
       float mx = z[0];
 #pragma unroll
-      for (int o = 1; o < NCLS; ++o) mx = fmaxf(mx, z[o]);
+      for (int o = 1; o < NCLS; ++o)
+        if (z[o] > mx) { mx = z[o]; am = o; }
+      float zy = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o) zy = (o == y) ? z[o] : zy;
       float s = 0.0f;
 #pragma unroll
       for (int o = 0; o < NCLS; ++o) { z[o] = expf(z[o] - mx); s += z[o]; }
-      const int y = labels[idx[(int64_t)r * bmax + jj]];
+      hl += (double)(logf(s) + mx - zy);
+      hc += (am == y) ? 1.0 : 0.0;
 #pragma unroll
       for (int o = 0; o < NCLS; ++o) dl_s[tid * NCLS + o] = (z[o] / s - (o == y ? 1.0f : 0.0f)) * inv_b;
     }
@@ -821,6 +833,20 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
           ((k & CODE_KEEP) && (k & CODE_POS)) ? acc * SCALE_50 : 0.0f;
     }
     __syncthreads();
+  }
+  if (hstats) {  // the step's training loss / accuracy sums before the update (Keras fit history)
+    hs_s[0][tid] = hl;
+    hs_s[1][tid] = hc;
+    __syncthreads();
+    for (int off = HEAD_CHUNK / 2; off >= 1; off >>= 1) {
+      if (tid < off) { hs_s[0][tid] += hs_s[0][tid + off]; hs_s[1][tid] += hs_s[1][tid + off]; }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      hstats[(int64_t)r * 3] = hs_s[0][0];
+      hstats[(int64_t)r * 3 + 1] = hs_s[1][0];
+      hstats[(int64_t)r * 3 + 2] = (double)count;
+    }
   }
   const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
   float* Rr = rms + (int64_t)r * STRIDE;
@@ -1150,7 +1176,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                   t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end);
   PROF_BEGIN(6);
   head_kernel<<<R, 256, 0, s>>>(t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5,
-                                t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
+                                t->lr, t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
   PROF_END(6);
   PROF_BEGIN(7);
   dense5_bwd_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,

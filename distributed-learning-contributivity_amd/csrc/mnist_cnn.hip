@@ -357,18 +357,24 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
                                                    const int32_t* __restrict__ adam_t, int bmax,
                                                    float* __restrict__ params, float* __restrict__ adam_m,
                                                    float* __restrict__ adam_v, int64_t stride,
-                                                   float* __restrict__ dH, float lr, float b1, float b2, float eps) {
+                                                   float* __restrict__ dH, float lr, float b1, float b2, float eps,
+                                                   double* __restrict__ hstats) {
   __shared__ float w4_s[HID * NCLS + NCLS];
   __shared__ float dl_s[HEAD_CHUNK * NCLS];
+  __shared__ double hs_s[2][HEAD_CHUNK];
   const int r = blockIdx.x;
   const int count = cnt[r];
-  if (count == 0) return;
   const int tid = threadIdx.x;
+  if (count == 0) {
+    if (hstats && tid < 3) hstats[(int64_t)r * 3 + tid] = 0.0;
+    return;
+  }
   float* P = params + (int64_t)r * stride;
   for (int e = tid; e < HID * NCLS + NCLS; e += 256) w4_s[e] = P[OFF_W4 + e];
   __syncthreads();
   const float inv_b = 1.0f / (float)count;
   float gacc[6] = {0, 0, 0, 0, 0, 0};  // dW4 elements tid, tid+256, ... (1290 = W4 + b4)
+  double hl = 0.0, hc = 0.0;           // this thread's training CE / correct sums (hstats)
   const float* Hr = H + (int64_t)r * bmax * HID;
   for (int c0 = 0; c0 < count; c0 += HEAD_CHUNK) {
     const int cn = min(HEAD_CHUNK, count - c0);
@@ -383,13 +389,20 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 #pragma unroll
         for (int o = 0; o < NCLS; ++o) z[o] += hv * w4_s[c * NCLS + o];
       }
+      const int y = labels[idx[(int64_t)r * bmax + jj]];
+      int am = 0;  // first maximum (the evaluation's argmax)
       float mx = z[0];
 #pragma unroll
-      for (int o = 1; o < NCLS; ++o) mx = fmaxf(mx, z[o]);
+      for (int o = 1; o < NCLS; ++o)
+        if (z[o] > mx) { mx = z[o]; am = o; }
+      float zy = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o) zy = (o == y) ? z[o] : zy;
       float s = 0.0f;
 #pragma unroll
       for (int o = 0; o < NCLS; ++o) { z[o] = expf(z[o] - mx); s += z[o]; }
-      const int y = labels[idx[(int64_t)r * bmax + jj]];
+      hl += (double)(logf(s) + mx - zy);
+      hc += (am == y) ? 1.0 : 0.0;
 #pragma unroll
       for (int o = 0; o < NCLS; ++o) dl_s[tid * NCLS + o] = (z[o] / s - (o == y ? 1.0f : 0.0f)) * inv_b;
     }
@@ -418,6 +431,20 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
       dH[((int64_t)r * bmax + c0 + jj) * HID + c] = hv > 0.0f ? a : 0.0f;
     }
     __syncthreads();
+  }
+  if (hstats) {  // the step's training loss / accuracy sums before the update (Keras fit history)
+    hs_s[0][tid] = hl;
+    hs_s[1][tid] = hc;
+    __syncthreads();
+    for (int off = HEAD_CHUNK / 2; off >= 1; off >>= 1) {
+      if (tid < off) { hs_s[0][tid] += hs_s[0][tid + off]; hs_s[1][tid] += hs_s[1][tid + off]; }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      hstats[(int64_t)r * 3] = hs_s[0][0];
+      hstats[(int64_t)r * 3 + 1] = hs_s[1][0];
+      hstats[(int64_t)r * 3 + 2] = (double)count;
+    }
   }
   const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
   float* Mr = adam_m + (int64_t)r * stride;
@@ -997,7 +1024,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   PROF_END(2);
   PROF_BEGIN(3);
   head_kernel<<<R, 256, 0, s>>>(t->hidden, t->idx, t->labels, t->cnt, t->adam_t, B, t->params, t->adam_m, t->adam_v,
-                                S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps);
+                                S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps, t->hstats);
   PROF_END(3);
   PROF_BEGIN(4);
   dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,

@@ -41,7 +41,8 @@ class CifarTrainT(ctypes.Structure):
                                                    "code4", "d5", "code5", "dh5", "dz4", "dz3", "dz2", "dz1", "wt",
                                                    "wpart")]
                 + [(n, ctypes.c_float) for n in ("lr", "rho", "one_minus_rho", "decay", "eps")]
-                + [("prof_kernel", ctypes.c_int32), ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p)])
+                + [("prof_kernel", ctypes.c_int32), ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p),
+                   ("hstats", ctypes.c_void_p)])
 
 
 _BOUND = False

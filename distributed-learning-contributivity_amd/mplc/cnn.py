@@ -62,7 +62,7 @@ class TrainT(ctypes.Structure):
                 ("w2_part", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("pad1", ctypes.c_int32),
-                ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p)]
+                ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p), ("hstats", ctypes.c_void_p)]
 
 KERNEL_IDS = {"conv_fwd": 1, "dense_fwd": 2, "head": 3, "dense1_bwd_adam": 4, "conv_bwd_data": 5, "conv_wgrad": 6,
               "adam_small": 7}
@@ -108,6 +108,33 @@ def shuffle_key(seed, mask, partner):
 def seq_order_key(seed, mask):
     """Key of the per-round member order of a sequential coalition (keyed.h seq_locate)."""
     return mix64(mix64((seed + 0x5E90) & M64) ^ mask)
+
+
+def subkey(key, a, b):
+    return mix64(key ^ mix64(((a << 32) | b) & M64))
+
+
+def keyed_perm(key, n, i):
+    """Host restatement of keyed.h keyed_perm: bijection of [0, n) (4-round Feistel + cycle walking)."""
+    if n <= 1:
+        return 0
+    h = ((n - 1).bit_length() + 1) >> 1
+    mask = (1 << h) - 1
+    x = i
+    while True:
+        L, R = x >> h, x & mask
+        for rd in range(4):
+            L, R = R, L ^ (mix64(key ^ (rd << 40) ^ R) & mask)
+        x = (L << h) | R
+        if x < n:
+            return x
+
+
+def seq_member_order(seed, mask, k, e, m):
+    """Member indices (ascending-partner order) of a sequential coalition in the visiting order of round
+    (e, m) (keyed.h seq_locate)."""
+    okey = subkey(seq_order_key(seed, mask), 0x60000 + e, m)
+    return [keyed_perm(okey, k, idx) for idx in range(k)]
 
 
 def _i32(v):
@@ -208,9 +235,10 @@ class TrainBatch:
     """Device state of one lockstep batch: coalition global rows, replica rows, optimizer state, workspaces
     (model-specific parts through eng.model_impl)."""
 
-    def __init__(self, eng, coalitions, epochs, lib):
+    def __init__(self, eng, coalitions, epochs, lib, record=False):
         import torch
         self.eng, self.lib = eng, lib
+        self.record = record
         self.model = eng.model_impl
         self.coalitions = coalitions
         self.epochs = epochs
@@ -285,11 +313,15 @@ class TrainBatch:
         self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
         self.seq_t = torch.tensor(seq_recs, **i32) if seq_recs else None
         self.snap = None
-        if seq_mode and self.approach != "seq-pure" and seq_recs:
+        if seq_mode and (self.approach != "seq-pure" or record) and seq_recs:
             # partner.model_weights of the aggregating variants: one snapshot row per (coalition, member)
             self.snap = torch.zeros((len(seq_recs) // SEQ_REC, S), **f32)
             self.snap_first_t = torch.tensor(snap_first, **i32)
         self.model.alloc(self)
+        self.hstats = None
+        if record:  # per-step training loss / accuracy sums of every replica (the head kernel's hstats)
+            self.hstats = torch.zeros((R, 3), dtype=torch.float64, device=dev)
+            self.t.hstats = self.hstats.data_ptr()
         self.stopped = np.zeros(C, dtype=bool)
         self.kind_host = self.rep_arr["kind"].copy()
         self.run_args = self.make_runs()
@@ -403,13 +435,20 @@ class CnnBatchTrainer:
         self.eng = engine
         self.lib = _native.lib()
 
-    def prepare(self, coalitions, epochs):
-        return TrainBatch(self.eng, coalitions, epochs, self.lib)
+    def prepare(self, coalitions, epochs, record=False):
+        return TrainBatch(self.eng, coalitions, epochs, self.lib, record=record)
 
-    def run(self, coalitions, epochs, early_stopping):
+    def run(self, coalitions, epochs, early_stopping, history=None):
+        """Train the coalitions in lockstep; returns (test accuracies, epochs done).  With `history` (a
+        dict, one coalition only) the learning history is recorded into it (HistoryRecorder)."""
         eng = self.eng
-        st = self.prepare(coalitions, epochs)
+        st = self.prepare(coalitions, epochs, record=history is not None)
         C = st.C
+        rec = None
+        if history is not None:
+            if C != 1:
+                raise ValueError("history recording takes exactly one coalition")
+            rec = HistoryRecorder(self, st, epochs, history)
         sizes = eng.partner_sizes
         fed = [ci for ci in range(C) if not st.coal_is_single[ci]]
         use_es = early_stopping and epochs > PATIENCE
@@ -424,13 +463,21 @@ class CnnBatchTrainer:
         for s in range(st.total_steps):
             if progress is not None and s % 30 == 0:
                 progress(s, st.total_steps, st.R)
-            if use_es and st.fed_steps and s % per_epoch_fed == 0 and s < st.fed_steps:
+            if rec is not None and st.fed_steps and s % st.round_len == 0 and s < st.fed_steps:
+                vl = rec.round_start(s)  # val of the round's start model (also the ES value at minibatch 0)
+                if use_es and s % per_epoch_fed == 0:
+                    val_hist[0].append(vl)
+            elif use_es and st.fed_steps and s % per_epoch_fed == 0 and s < st.fed_steps:
                 live = [ci for ci in fed if not st.stopped[ci]]
                 if live:  # val loss of each live global model at the start of epoch e (minibatch 0)
                     for ci, l in zip(live, self._val_loss(st.glob, live)):
                         val_hist[ci].append(l)
             st.step(s)
+            if rec is not None:
+                rec.after_step(s)
             if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                if rec is not None:
+                    rec.round_end(s)
                 st.aggregate(epoch_end=(s + 1) % per_epoch_fed == 0)
                 if use_es and (s + 1) % per_epoch_fed == 0:
                     e = (s + 1) // per_epoch_fed - 1
@@ -454,6 +501,8 @@ class CnnBatchTrainer:
                                 st.stop(ci)
             if st.stopped.all():
                 break
+        if rec is not None:
+            rec.finish(epochs_done[0])
         glob = st.finalize()
         correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
         return correct / float(eng.y_test_d.numel()), epochs_done
@@ -467,3 +516,100 @@ class CnnBatchTrainer:
     def _val_loss(self, params, rows):
         _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)
         return [float(v) for v in loss]
+
+
+class HistoryRecorder:
+    """The learning history of one coalition's training (mplc/mpl_utils.py:11-27 History.history):
+    'mpl_model' val_loss / val_accuracy [E, M] of the round-start global model (eval_and_log_model_val_perf,
+    called at the start of every round, mplc/multi_partner_learning.py:142-156, 319-320, 363-364) and, per
+    partner, the Keras fit history of its round (log_partner_perf, :130-133): 'loss' / 'accuracy' are the
+    running training values of the fit (per-sample CE and correct predictions before each update, from
+    the head kernel's hstats), 'val_loss' / 'val_accuracy' those of the partner's model after the fit.
+    A singleton (SinglePartnerLearning, :238-269) logs its last epoch at [0, 0] and has no 'mpl_model'.
+    Unvisited entries keep the reference's initial values (NaN for partners, 0 for the collective model)."""
+    METRICS = ("val_accuracy", "val_loss", "loss", "accuracy")
+
+    def __init__(self, trainer, st, epochs, out):
+        eng = trainer.eng
+        self.trainer, self.st, self.eng = trainer, st, eng
+        self.coal = st.coalitions[0]
+        self.k = len(self.coal)
+        self.M = eng.minibatch_count
+        self.mask = sum(1 << p for p in self.coal)
+        self.n_val = float(eng.y_val_d.numel())
+        self.h = out
+        for p in self.coal:
+            out[p] = {m: np.full((epochs, self.M), np.nan) for m in self.METRICS}
+        if self.k > 1:
+            out["mpl_model"] = {"val_accuracy": np.zeros((epochs, self.M)), "val_loss": np.zeros((epochs, self.M))}
+        self.acc = np.zeros((self.k, 3))
+        self.single_spe = None
+        if self.k == 1:
+            p = self.coal[0]
+            self.single_spe = -(-eng.partner_sizes[p] // eng.batch_sizes[p])
+            self.last = None
+        self.order_steps = None
+
+    def _val(self, params, rows):
+        correct, loss = self.trainer._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)
+        return correct / self.n_val, loss
+
+    def round_start(self, s):
+        e, m = divmod(s // self.st.round_len, self.M)
+        acc, loss = self._val(self.st.glob, [0])
+        self.h["mpl_model"]["val_accuracy"][e, m] = acc[0]
+        self.h["mpl_model"]["val_loss"][e, m] = loss[0]
+        self.acc[:] = 0.0
+        if self.st.seq_mode:  # member visiting order and fit lengths of this round
+            b = self.eng.bounds
+            order = seq_member_order(self.eng.seed, self.mask, self.k, e, m)
+            self.order_steps = []
+            for mi in order:
+                p = self.coal[mi]
+                self.order_steps.extend([mi] * (-(-(b[p][m + 1] - b[p][m]) // self.eng.batch_sizes[p])))
+        return float(loss[0])
+
+    def after_step(self, s):
+        hs = self.st.hstats.cpu().numpy()
+        if self.k == 1:
+            t = s % self.single_spe
+            if t == 0:
+                self.acc[:] = 0.0
+            self.acc[0] += hs[0]
+            if t == self.single_spe - 1 and s // self.single_spe < self.st.epochs:
+                self.last = self.acc[0].copy()  # the epoch's running loss / accuracy
+            return
+        if s >= self.st.fed_steps:
+            return
+        if self.st.seq_mode:
+            t = s % self.st.round_len
+            if t < len(self.order_steps):
+                self.acc[self.order_steps[t]] += hs[0]
+        else:
+            self.acc += hs[:self.k]
+
+    def round_end(self, s):
+        e, m = divmod(s // self.st.round_len, self.M)
+        st = self.st
+        if st.seq_mode:
+            base = st.snap_row(0)
+            acc, loss = self._val(st.snap, [base + mi for mi in range(self.k)])
+        else:
+            acc, loss = self._val(st.params, list(range(st.coal_first[0], st.coal_first[0] + self.k)))
+        for mi, p in enumerate(self.coal):
+            h = self.h[p]
+            n = self.acc[mi, 2]
+            h["val_accuracy"][e, m] = acc[mi]
+            h["val_loss"][e, m] = loss[mi]
+            h["loss"][e, m] = self.acc[mi, 0] / n if n else np.nan
+            h["accuracy"][e, m] = self.acc[mi, 1] / n if n else np.nan
+
+    def finish(self, epochs_done):
+        if self.k != 1 or self.last is None:
+            return
+        p = self.coal[0]
+        acc, loss = self._val(self.st.params, [self.st.coal_first[0]])
+        h = self.h[p]
+        h["val_accuracy"][0, 0], h["val_loss"][0, 0] = acc[0], loss[0]
+        h["loss"][0, 0] = self.last[0] / self.last[2]
+        h["accuracy"][0, 0] = self.last[1] / self.last[2]

@@ -790,9 +790,62 @@ class Contributivity:
         self._finish("WR_SMC Shapley", shap, np.sqrt(var))
 
     # --------------------------------------------------------------------------------------------
+    # Federated step-by-step scores (mplc/contributivity.py:1015-1115): post-processing of the recorded
+    # history of the scenario's main learning run (scenario.mpl, Scenario.run); no coalition evaluations
+    # --------------------------------------------------------------------------------------------
+    def compute_relative_perf_matrix(self):
+        """Per kept round (the first and last 10 % of the E*M rounds are skipped), each partner's
+        val_accuracy after its fit divided by the round-start collective model's val_accuracy
+        (mplc/contributivity.py:1079-1115).  Shape [kept rounds, partners]."""
+        mpl = getattr(self.scenario, "mpl", None)
+        hist = getattr(getattr(mpl, "history", None), "history", None)
+        if not hist or "mpl_model" not in hist:
+            raise RuntimeError("the Federated SBS methods read the learning history of the scenario's main "
+                               "multi-partner run: call Scenario.run() (or fit a learner with record_history=True)")
+        collective = np.asarray(hist["mpl_model"]["val_accuracy"])
+        # [partners, E, M] -> [E, M, partners] as axis swaps (a strided view: the memory layout, and with it
+        # the summation order of the score dot products below, is the reference's)
+        per_partner = np.swapaxes(np.swapaxes([v["val_accuracy"] for k, v in hist.items() if k != "mpl_model"],
+                                              0, 2), 0, 1)
+        E, M = mpl.epoch_count, mpl.minibatch_count
+        first = int(np.round(E * M * 0.1))
+        last = int(np.round(E * M * (1 - 0.1)))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rel = np.divide(np.reshape(per_partner, (E * M, mpl.partners_count)),
+                            np.reshape(collective, (E * M))[:, None])
+        return rel[first:last, :]
+
+    def _sbs(self, name, scores):
+        self.name = name
+        self.contributivity_scores = scores
+        self.normalized_scores = self.contributivity_scores / np.sum(self.contributivity_scores)
+
+    def federated_SBS_linear(self):
+        start = timer()
+        rel = self.compute_relative_perf_matrix()
+        self._sbs("Federated step by step linear scores", np.arange(rel.shape[0]).dot(np.nan_to_num(rel)))
+        self.computation_time_sec = timer() - start
+
+    def federated_SBS_quadratic(self):
+        start = timer()
+        rel = self.compute_relative_perf_matrix()
+        self._sbs("Federated step by step quadratic scores",
+                  np.square(np.arange(rel.shape[0])).dot(np.nan_to_num(rel)))
+        self.computation_time_sec = timer() - start
+
+    def federated_SBS_constant(self):
+        start = timer()
+        rel = self.compute_relative_perf_matrix()
+        with np.errstate(invalid="ignore"):
+            self._sbs("Federated step by step constant scores", np.nanmean(rel, axis=0))
+        self.computation_time_sec = timer() - start
+
+    # --------------------------------------------------------------------------------------------
     # Dispatcher (mplc/contributivity.py:1134-1198)
     # --------------------------------------------------------------------------------------------
-    OUT_OF_SCOPE = ("Federated SBS linear", "Federated SBS quadratic", "Federated SBS constant", "PVRL", "LFlip")
+    OUT_OF_SCOPE = ("PVRL", "LFlip")
+    SBS = {"Federated SBS linear": "federated_SBS_linear", "Federated SBS quadratic": "federated_SBS_quadratic",
+           "Federated SBS constant": "federated_SBS_constant"}
 
     def compute_contributivity(self, method_to_compute, sv_accuracy=0.01, alpha=0.95, truncation=0.05,
                                update=50):
@@ -809,10 +862,16 @@ class Contributivity:
         }
         if method_to_compute in dispatch:
             dispatch[method_to_compute]()
+        elif method_to_compute in self.SBS:
+            approach = getattr(self.scenario, "multi_partner_learning_approach", None)
+            if approach is not multi_partner_learning.FederatedAverageLearning:
+                logger.warning(f"{method_to_compute}: step by step contributivity methods are only suited for "
+                               "federated averaging learning approach")
+            getattr(self, self.SBS[method_to_compute])()
         elif method_to_compute in self.OUT_OF_SCOPE:
             raise NotImplementedError(
-                f"'{method_to_compute}' makes no coalition evaluations (it post-processes one learning history, "
-                "or is broken in the reference); it is outside this engine's scope (DESIGN.md)")
+                f"'{method_to_compute}' trains its own modified learner (label-flip / partner-selection policy) "
+                "instead of evaluating coalitions; it is outside this engine's scope (DESIGN.md)")
         else:
             logger.warning("Unrecognized name of method, statement ignored!")
 

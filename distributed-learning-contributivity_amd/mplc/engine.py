@@ -158,8 +158,12 @@ class CoalitionEngine:
         self.model_impl.init_params(buf, keys, _native.stream_handle(self.device))
         torch.cuda.synchronize(self.device)
 
-    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):
-        """v(S) (test accuracy, float64) for each coalition (sorted tuple of partner indices)."""
+    supports_history = True
+
+    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
+                 record_history=False):
+        """v(S) (test accuracy, float64) for each coalition (sorted tuple of partner indices).  With
+        record_history (one coalition) the details also hold its learning history (cnn.HistoryRecorder)."""
         coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
         for c in coalitions:
             if len(c) == 0 or c[0] < 0 or c[-1] >= len(self.partner_sizes) or len(set(c)) != len(c):
@@ -168,9 +172,14 @@ class CoalitionEngine:
         es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
         scores = np.zeros(len(coalitions))
         epochs_done = np.zeros(len(coalitions), dtype=np.int64)
+        history = None
+        if record_history:
+            if len(coalitions) != 1:
+                raise ValueError("record_history takes exactly one coalition")
+            history = {}
         for batch in self.plan_batches(coalitions):
             coal = [coalitions[i] for i in batch]
-            s, e = self.trainer.run(coal, E, es)
+            s, e = self.trainer.run(coal, E, es, history=history)
             scores[batch] = s
             epochs_done[batch] = e
             self.stats["batches"] += 1
@@ -180,7 +189,10 @@ class CoalitionEngine:
                                              for c, ep in zip(coal, e)))
         self.stats["coalitions"] += len(coalitions)
         if return_details:
-            return {"scores": scores, "epochs_done": epochs_done}
+            out = {"scores": scores, "epochs_done": epochs_done}
+            if history is not None:
+                out["history"] = history
+            return out
         return scores
 
 

@@ -19,12 +19,37 @@ ALLOWED_PARAMETERS = ('partners_list', 'epoch_count', 'minibatch_count', 'datase
 
 
 class History:
-    """Subset of mplc/mpl_utils.py:11-27 that the coalition path reads: score and nb_epochs_done."""
+    """mplc/mpl_utils.py:11-45: score (test accuracy of the final model), nb_epochs_done, and the learning
+    history ``history[partner_id][metric]`` / ``history['mpl_model'][metric]`` as [epoch_count,
+    minibatch_count] arrays (partners: 'val_accuracy', 'val_loss', 'loss', 'accuracy', NaN until logged;
+    the collective model: 'val_accuracy', 'val_loss', zeros until logged).  Filled by a recorded fit
+    (MultiPartnerLearning.fit with record_history, the scenario's main learning run); a fit served from
+    the coalition-value cache leaves it empty."""
+    metrics = ['val_accuracy', 'val_loss', 'loss', 'accuracy']
 
-    def __init__(self):
+    def __init__(self, mpl=None):
+        self.mpl = mpl
+        self.save_folder = getattr(mpl, "save_folder", None)
         self.score = None
         self.nb_epochs_done = 0
         self.history = {}
+
+    def partners_to_dataframe(self):
+        """mplc/mpl_utils.py:29-43: one row per (partner, epoch, minibatch) with the four metrics."""
+        import pandas as pd
+        temp = {'Partner': [], 'Epoch': [], 'Minibatch': []}
+        for key in self.metrics:
+            temp[key] = []
+        for pid, hist in [(k, v) for k, v in self.history.items() if k != 'mpl_model']:
+            E, M = next(iter(hist.values())).shape
+            for epoch in range(E):
+                for mb in range(M):
+                    temp['Partner'].append(pid)
+                    temp['Epoch'].append(epoch)
+                    temp['Minibatch'].append(mb)
+                    for metric, matrix in hist.items():
+                        temp[metric].append(matrix[epoch, mb])
+        return pd.DataFrame.from_dict(temp)
 
 
 def _engine(scenario):
@@ -57,7 +82,8 @@ class MultiPartnerLearning:
         self.epoch_index = 0
         self.minibatch_index = 0
         self.learning_computation_time = 0
-        self.history = History()
+        self.record_history = bool(kwargs.get("record_history", False))
+        self.history = History(self)
 
     @property
     def partners_count(self):
@@ -74,16 +100,21 @@ class MultiPartnerLearning:
         # (mplc/contributivity.py:100-112); reuse it only for a fit with the same semantics
         same = (self.epoch_count == getattr(self.scenario, "epoch_count", self.epoch_count)
                 and (self.is_early_stopping or self.epoch_count <= constants.PATIENCE))
-        if same and cache is not None and key in cache:  # evaluated earlier (or loaded from a persisted table)
+        if same and cache is not None and key in cache and not self.record_history:  # evaluated earlier (or persisted)
             self.history.score = float(cache[key])
             self.history.nb_epochs_done = int(getattr(self.scenario, "coalition_epochs", {}).get(key, self.epoch_count))
             self.learning_computation_time = timer() - start
             return
         eng = _engine(self.scenario)
+        record = self.record_history and getattr(eng, "supports_history", False)
+        kw = dict(record_history=True) if record else {}
         res = eng.evaluate([self._coalition()], epoch_count=self.epoch_count,
-                           is_early_stopping=self.is_early_stopping, return_details=True)
+                           is_early_stopping=self.is_early_stopping, return_details=True, **kw)
         self.history.score = float(res["scores"][0])
         self.history.nb_epochs_done = int(res["epochs_done"][0])
+        if record:  # keyed by partner.id (== the engine's partner index) and 'mpl_model'
+            self.history.history = res["history"]
+            self.epoch_index = self.history.nb_epochs_done - 1
         self.learning_computation_time = timer() - start
 
     # Contributivity plans TMCS/ITMCS permutation waves with the device walk (mplc.mc) for this approach

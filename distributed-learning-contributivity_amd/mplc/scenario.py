@@ -184,7 +184,9 @@ class Scenario:
         self.provision()
         if self.coalition_values_file:
             self.load_coalition_values(self.coalition_values_file, missing_ok=True)
-        self.mpl = self.multi_partner_learning_approach(self, is_save_data=True)
+        # the main learning run records its history (mplc/mpl_utils.py:11-27), which the Federated SBS
+        # methods read (mplc/contributivity.py:1079-1115)
+        self.mpl = self.multi_partner_learning_approach(self, is_save_data=True, record_history=True)
         self.mpl.fit()
         if self.is_early_stopping or self.epoch_count <= constants.PATIENCE:  # same v(N) as Contributivity's
             self.coalition_values[tuple(range(self.partners_count))] = self.mpl.history.score

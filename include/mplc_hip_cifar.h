@@ -111,6 +111,10 @@ typedef struct {
   int32_t prof_kernel;
   void* prof_begin;
   void* prof_end;
+  /* optional training history (NULL = off): per replica, the step's [sum of per-sample CE before the
+   * update, correct predictions, samples] (dropout active, as a Keras fit reports them); see
+   * mplc_cnn_train_t.hstats */
+  double* hstats;         /* [n_rep][3]                                                   */
 } mplc_cifar_train_t;
 
 /* Parameter row stride in floats (== MPLC_CIFAR_STRIDE). */

@@ -114,6 +114,10 @@ typedef struct {
   int32_t pad1;
   void* prof_begin;
   void* prof_end;
+  /* optional training history (NULL = off): per replica, the step's [sum of per-sample CE before the
+   * update, correct predictions, samples] - the running 'loss' / 'accuracy' that a Keras fit reports
+   * (mplc/multi_partner_learning.py:130-133 log_partner_perf); idle replicas write zeros */
+  double* hstats;         /* [n_rep][3]                                                   */
 } mplc_cnn_train_t;
 
 /* Parameter row stride in floats (== MPLC_CNN_STRIDE). */

@@ -259,23 +259,59 @@ def average_models(glob, models, w):
     return new
 
 
+class _FitLog:
+    """Keras fit history of one fit: running training CE / accuracy over the fit's batches (each batch's
+    values before its update, sample-weighted), then val metrics of the fitted model
+    (mplc/multi_partner_learning.py:130-133 log_partner_perf; mplc/mpl_utils.py:11-27)."""
+
+    def __init__(self):
+        self.loss, self.correct, self.n = 0.0, 0, 0
+
+    def batch(self, params, x, y, loss_mean):
+        torch = _torch()
+        with torch.no_grad():
+            self.correct += int((forward(params, x).argmax(1) == y).sum())
+        self.loss += loss_mean * len(y)
+        self.n += len(y)
+
+    def store(self, h, e, m, params, data):
+        vl, va = evaluate(params, data.x_val, data.y_val)
+        h["val_loss"][e, m], h["val_accuracy"][e, m] = vl, va
+        h["loss"][e, m] = self.loss / self.n if self.n else np.nan
+        h["accuracy"][e, m] = self.correct / self.n if self.n else np.nan
+
+
+HISTORY_METRICS = ("val_accuracy", "val_loss", "loss", "accuracy")
+
+
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
-                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg"):
-    """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init and order."""
+                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg",
+                    history=None):
+    """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init and order.
+    With a `history` dict, the learning history (mplc/mpl_utils.py:11-27) is recorded into it."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
     mask = sum(1 << p for p in coalition)
     glob = unpack(init_params(init_key(seed, mask)))
     epochs_done = epochs
+    if history is not None:
+        for p_id in coalition:
+            history[p_id] = {k: np.full((epochs, M), np.nan) for k in HISTORY_METRICS}
+        if len(coalition) > 1:
+            history["mpl_model"] = {"val_accuracy": np.zeros((epochs, M)), "val_loss": np.zeros((epochs, M))}
     if len(coalition) == 1:
         p_id = coalition[0]
         key = shuffle_key(seed, mask, p_id)
         params = {k: v.clone() for k, v in glob.items()}
         opt = KerasAdam(params)
         best, wait = np.inf, 0
+        log = None
         for e in range(epochs):
+            log = _FitLog() if history is not None else None
             for rows in single_epoch_rows(key, partner_rows[p_id], batch_sizes[p_id], e):
-                g, _ = gradients(params, data.x_train[rows], data.y_train[rows])
+                g, lm = gradients(params, data.x_train[rows], data.y_train[rows])
+                if log is not None:
+                    log.batch(params, data.x_train[rows], data.y_train[rows], lm)
                 opt.step(params, g)
             if early_stopping and epochs > PATIENCE:
                 vl, _ = evaluate(params, data.x_val, data.y_val)
@@ -287,6 +323,8 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                         epochs_done = e + 1
                         break
         glob = params
+        if log is not None:  # SinglePartnerLearning logs the last epoch at [0, 0]
+            log.store(history[p_id], 0, 0, params, data)
     else:
         sizes = [len(partner_rows[p]) for p in coalition]
         if aggregation == "uniform":
@@ -298,6 +336,9 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
             if early_stopping and epochs > PATIENCE:
                 val_hist.append(evaluate(glob, data.x_val, data.y_val)[0])
             for m in range(M):
+                if history is not None:  # round-start collective model (eval_and_log_model_val_perf)
+                    vl, va = evaluate(glob, data.x_val, data.y_val)
+                    history["mpl_model"]["val_loss"][e, m], history["mpl_model"]["val_accuracy"][e, m] = vl, va
                 if approach != "fedavg":
                     # seq-pure / seq-with-final-agg / seqavg (mplc/multi_partner_learning.py:337-433): one model
                     # and one optimizer per round, members in the round's shuffled order, snapshots per member
@@ -307,10 +348,15 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                     for mi in seq_member_order(seed, mask, len(coalition), e, m):
                         p_id = coalition[mi]
                         key = shuffle_key(seed, mask, p_id)
+                        log = _FitLog() if history is not None else None
                         for rows in fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m):
-                            g, _ = gradients(params, data.x_train[rows], data.y_train[rows])
+                            g, lm = gradients(params, data.x_train[rows], data.y_train[rows])
+                            if log is not None:
+                                log.batch(params, data.x_train[rows], data.y_train[rows], lm)
                             opt.step(params, g)
                         snaps[mi] = {k: v.clone() for k, v in params.items()}
+                        if log is not None:
+                            log.store(history[p_id], e, m, params, data)
                     if approach == "seqavg" or (approach == "seq-with-final-agg" and m == M - 1):
                         glob = average_models(glob, snaps, w)
                     else:
@@ -321,9 +367,14 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                     key = shuffle_key(seed, mask, p_id)
                     params = {k: v.clone() for k, v in glob.items()}
                     opt = KerasAdam(params)  # fresh optimizer per partner fit
+                    log = _FitLog() if history is not None else None
                     for rows in fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m):
-                        g, _ = gradients(params, data.x_train[rows], data.y_train[rows])
+                        g, lm = gradients(params, data.x_train[rows], data.y_train[rows])
+                        if log is not None:
+                            log.batch(params, data.x_train[rows], data.y_train[rows], lm)
                         opt.step(params, g)
+                    if log is not None:
+                        log.store(history[p_id], e, m, params, data)
                     partner_models.append(params)
                 glob = average_models(glob, partner_models, w)
             if early_stopping and epochs > PATIENCE and e >= PATIENCE and val_hist[e] > val_hist[e - PATIENCE]:

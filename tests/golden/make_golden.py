@@ -17,6 +17,8 @@ Fixtures written (all data, no reference source):
   splits.json          - mplc/scenario.py:571-724 + mplc/dataset.py:62-106 partner index arrays and bs_p
   fedavg_lr.json       - mplc/multi_partner_learning.py:195-334 FedAvg with the Titanic LogisticRegression
                          model (mplc/dataset.py:323-394) on synthetic Titanic-shaped data: v(S) per coalition
+  sbs.json             - mplc/contributivity.py:1015-1115 Federated SBS linear / quadratic / constant on seeded
+                         learning histories
 """
 import itertools
 import json
@@ -317,11 +319,50 @@ def gen_fedavg_lr(mplc):
     return out
 
 
+# --------------------------------------------------------------------------------------------------
+# (e) Federated step-by-step scores on synthetic learning histories
+# --------------------------------------------------------------------------------------------------
+def gen_sbs(mplc):
+    """mplc/contributivity.py:1015-1115 on seeded History.history dicts (partners' val_accuracy per
+    (epoch, minibatch), NaN where unlogged; the collective model's val_accuracy, 0 where unlogged)."""
+    out = []
+    for case, (P, E, M, stop, holes) in enumerate(((3, 3, 4, None, 0), (4, 5, 6, 3, 3), (2, 2, 10, None, 2),
+                                                    (5, 1, 7, None, 0), (3, 4, 5, 2, 0))):
+        rng = np.random.default_rng(500 + case)
+        coll = np.zeros((E, M))
+        parts = [np.full((E, M), np.nan) for _ in range(P)]
+        done = E if stop is None else stop
+        coll[:done] = rng.uniform(0.1, 0.95, size=(done, M))
+        for p in range(P):
+            parts[p][:done] = rng.uniform(0.05, 0.95, size=(done, M))
+        for _ in range(holes):  # partners with no fit logged in a round
+            parts[int(rng.integers(P))][int(rng.integers(done)), int(rng.integers(M))] = np.nan
+        hist = {i: {"val_accuracy": parts[i]} for i in range(P)}
+        hist["mpl_model"] = {"val_accuracy": coll}
+        mpl = types.SimpleNamespace(history=types.SimpleNamespace(history=hist), partners_count=P,
+                                    epoch_count=E, minibatch_count=M)
+        partners = [types.SimpleNamespace(id=i) for i in range(P)]
+        scenario = types.SimpleNamespace(partners_list=partners, mpl=mpl,
+                                         multi_partner_learning_approach=mplc.multi_partner_learning.FederatedAverageLearning)
+        res = {"P": P, "E": E, "M": M, "collective": coll.tolist(), "partners": [x.tolist() for x in parts]}
+        for method in ("Federated SBS linear", "Federated SBS quadratic", "Federated SBS constant"):
+            contrib = mplc.contributivity.Contributivity(scenario=scenario)
+            with np.errstate(all="ignore"):
+                contrib.compute_contributivity(method)
+            res[method] = {"name": contrib.name,
+                           "scores": [float(x) for x in np.atleast_1d(contrib.contributivity_scores)],
+                           "normalized": [float(x) for x in np.atleast_1d(contrib.normalized_scores)],
+                           "std": [float(x) for x in np.atleast_1d(contrib.scores_std)]}
+        out.append(res)
+        print(f"sbs case {case}: P={P} E={E} M={M}", flush=True)
+    return out
+
+
 def main():
     only = set(sys.argv[1:])
     mplc = import_reference()
     jobs = {"shapley_value": gen_shapley, "estimators": gen_estimators, "splits": gen_splits,
-            "fedavg_lr": gen_fedavg_lr}
+            "fedavg_lr": gen_fedavg_lr, "sbs": gen_sbs}
     for name, fn in jobs.items():
         if only and name not in only:
             continue
