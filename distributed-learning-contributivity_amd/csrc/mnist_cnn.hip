@@ -206,23 +206,35 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   floatx16 acc[3][2];
 #pragma unroll
   for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
-  const float* W2 = P + OFF_W2;
-  for (int kyx = 0; kyx < 9; ++kyx) {
-    const int ky = kyx / 3, kx = kyx % 3;
-    const int off = (ky * A1 + kx) * A1P;
-    const float* w2k = W2 + (int64_t)kyx * C1 * C2;
-#pragma unroll 8
-    for (int c2 = 0; c2 < 16; ++c2) {
-      const int ci = 2 * c2 + kh;
-      const float b0 = w2k[ci * C2 + m];
-      const float b1 = w2k[ci * C2 + 32 + m];
+  // K = 9 taps x 32 channels in 18 groups of 8 channel pairs; the B operand (W2, L2-resident) of group g + 1
+  // is loaded into registers while group g's 48 MFMAs run
+  const float* W2 = P + OFF_W2 + kh * C2 + m;
+  float bcur[16], bnxt[16];
+  auto load_b = [&](int g, float (&b)[16]) {
+    const float* w = W2 + (int64_t)((g >> 1) * C1 + (g & 1) * 16) * C2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      b[2 * i] = w[2 * i * C2];
+      b[2 * i + 1] = w[2 * i * C2 + 32];
+    }
+  };
+  load_b(0, bcur);
+#pragma unroll
+  for (int g = 0; g < 18; ++g) {
+    if (g + 1 < 18) load_b(g + 1, bnxt);
+    const int kyx = g >> 1, ky = kyx / 3, kx = kyx % 3;
+    const int off = (ky * A1 + kx) * A1P + (g & 1) * 16 + kh;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const float a = a1_s[pbase[u] + off + ci];
-        acc[u][0] = mfma32(a, b0, acc[u][0]);
-        acc[u][1] = mfma32(a, b1, acc[u][1]);
+        const float a = a1_s[pbase[u] + off + 2 * i];
+        acc[u][0] = mfma32(a, bcur[2 * i], acc[u][0]);
+        acc[u][1] = mfma32(a, bcur[2 * i + 1], acc[u][1]);
       }
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bcur[i] = bnxt[i];
   }
   // epilogue: bias, ReLU, 2x2 max-pool (first max in window scan order), argmax code
   float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
