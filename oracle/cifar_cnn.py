@@ -197,14 +197,40 @@ class Data:
         self.x_test, self.y_test = img(x_test), lab(y_test)
 
 
+class _FitLog(ocnn._FitLog):
+    """Keras fit history of one fit (see oracle/cnn.py _FitLog): the training forward runs with the step's
+    dropout masks, as Keras' fit reports it; val metrics in inference mode."""
+
+    def batch(self, params, x, y, loss_mean, masks=None):
+        torch = _torch()
+        with torch.no_grad():
+            self.correct += int((forward(params, x, masks).argmax(1) == y).sum())
+        self.loss += loss_mean * len(y)
+        self.n += len(y)
+
+    def store(self, h, e, m, params, data):
+        vl, va = evaluate(params, data.x_val, data.y_val)
+        h["val_loss"][e, m], h["val_accuracy"][e, m] = vl, va
+        h["loss"][e, m] = self.loss / self.n if self.n else np.nan
+        h["accuracy"][e, m] = self.correct / self.n if self.n else np.nan
+
+
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
-                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg"):
-    """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init, order and masks."""
+                    aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg",
+                    history=None):
+    """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init, order and masks.
+    With a `history` dict, the learning history (mplc/mpl_utils.py:11-27) is recorded into it."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
     mask = sum(1 << p for p in coalition)
     glob = unpack(init_params(ocnn.init_key(seed, mask)))
     epochs_done = epochs
+    if history is not None:
+        for p_id in coalition:
+            history[p_id] = {k: np.full((epochs, M), np.nan) for k in ocnn.HISTORY_METRICS}
+        if len(coalition) > 1:
+            history["mpl_model"] = {"val_accuracy": np.zeros((epochs, M)), "val_loss": np.zeros((epochs, M))}
+    log = None
     if len(coalition) == 1:
         p_id = coalition[0]
         key = ocnn.shuffle_key(seed, mask, p_id)
@@ -212,9 +238,12 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
         opt = KerasRMSprop(params)
         best, wait = np.inf, 0
         for e in range(epochs):
+            log = _FitLog() if history is not None else None
             for t, rows in enumerate(ocnn.single_epoch_rows(key, partner_rows[p_id], batch_sizes[p_id], e)):
                 masks = step_masks(single_drop_key(key, e, t), len(rows))
-                g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                g, lm = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                if log is not None:
+                    log.batch(params, data.x_train[rows], data.y_train[rows], lm, masks)
                 opt.step(params, g)
             if early_stopping and epochs > PATIENCE:
                 vl, _ = evaluate(params, data.x_val, data.y_val)
@@ -226,6 +255,8 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                         epochs_done = e + 1
                         break
         glob = params
+        if log is not None:  # SinglePartnerLearning logs the last epoch at [0, 0]
+            log.store(history[p_id], 0, 0, params, data)
     else:
         sizes = [len(partner_rows[p]) for p in coalition]
         w = [1 / len(coalition)] * len(coalition) if aggregation == "uniform" else np.asarray(sizes) / np.sum(sizes)
@@ -234,6 +265,9 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
             if early_stopping and epochs > PATIENCE:
                 val_hist.append(evaluate(glob, data.x_val, data.y_val)[0])
             for m in range(M):
+                if history is not None:  # round-start collective model (eval_and_log_model_val_perf)
+                    vl, va = evaluate(glob, data.x_val, data.y_val)
+                    history["mpl_model"]["val_loss"][e, m], history["mpl_model"]["val_accuracy"][e, m] = vl, va
                 if approach != "fedavg":  # sequential approaches, as oracle/cnn.py
                     params = {k: v.clone() for k, v in glob.items()}
                     opt = KerasRMSprop(params)
@@ -242,11 +276,16 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                         p_id = coalition[mi]
                         key = ocnn.shuffle_key(seed, mask, p_id)
                         steps = ocnn.fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m)
+                        log = _FitLog() if history is not None else None
                         for t, rows in enumerate(steps):
                             masks = step_masks(fedavg_drop_key(key, e, m, t), len(rows))
-                            g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                            g, lm = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                            if log is not None:
+                                log.batch(params, data.x_train[rows], data.y_train[rows], lm, masks)
                             opt.step(params, g)
                         snaps[mi] = {k: v.clone() for k, v in params.items()}
+                        if log is not None:
+                            log.store(history[p_id], e, m, params, data)
                     if approach == "seqavg" or (approach == "seq-with-final-agg" and m == M - 1):
                         glob = ocnn.average_models(glob, snaps, w)
                     else:
@@ -258,10 +297,15 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                     params = {k: v.clone() for k, v in glob.items()}
                     opt = KerasRMSprop(params)  # fresh optimizer per partner fit
                     steps = ocnn.fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m)
+                    log = _FitLog() if history is not None else None
                     for t, rows in enumerate(steps):
                         masks = step_masks(fedavg_drop_key(key, e, m, t), len(rows))
-                        g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                        g, lm = gradients(params, data.x_train[rows], data.y_train[rows], masks)
+                        if log is not None:
+                            log.batch(params, data.x_train[rows], data.y_train[rows], lm, masks)
                         opt.step(params, g)
+                    if log is not None:
+                        log.store(history[p_id], e, m, params, data)
                     partner_models.append(params)
                 new = {}
                 for k in glob:

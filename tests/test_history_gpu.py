@@ -54,8 +54,8 @@ def compare(dev, ref, coal):
         if "mpl_model" in ref else None
     if "mpl_model" in ref:
         assert abs(dev["mpl_model"]["val_accuracy"][0, 0] - ref["mpl_model"]["val_accuracy"][0, 0]) <= 2.5e-3
-    for p in coal:
-        np.testing.assert_allclose(dev[p]["loss"][0, 0], ref[p]["loss"][0, 0], rtol=1e-4)
+    for p in coal:  # round 0's fits: a few optimizer steps (after other members' fits when sequential)
+        np.testing.assert_allclose(dev[p]["loss"][0, 0], ref[p]["loss"][0, 0], rtol=1e-3)
     # every entry: accuracies within 3 points, +-1 point on average; losses within 15 %
     accs = []
     for k in ref:
@@ -122,23 +122,23 @@ def test_scenario_run_history_and_federated_sbs():
     assert abs(np.sum(const.normalized_scores) - 1.0) < 1e-12
 
 
-def test_cifar_history_records():
+@pytest.mark.parametrize("approach", ("fedavg", "seqavg"))
+def test_cifar_history_vs_oracle(approach):
     from mplc.dataset import ArrayDataset, digits_as_cifar
     from mplc.scenario import Scenario
+    from oracle import cifar_cnn as occ
     x, y = digits_as_cifar()
     ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:], name="cifar10")
     sc = Scenario(3, [0.2, 0.5, 0.3], dataset=ds, minibatch_count=2, gradient_updates_per_pass_count=4, epoch_count=2,
-                  is_early_stopping=False).provision()
+                  is_early_stopping=False, multi_partner_learning_approach=approach).provision()
     eng = engine_for(sc)
-    res = eng.evaluate([(0, 1, 2)], return_details=True, record_history=True)
-    h = res["history"]
-    assert set(h) == {0, 1, 2, "mpl_model"}
-    for p in range(3):
-        for metric in METRICS:
-            v = h[p][metric]
-            assert not np.isnan(v).any()
-            if metric.endswith("accuracy"):
-                assert np.all((v >= 0) & (v <= 1))
-            else:
-                assert np.all(v > 0)
-    assert eng.evaluate([(0, 1, 2)])[0] == res["scores"][0]
+    coal = (0, 1, 2)
+    res = eng.evaluate([coal], return_details=True, record_history=True)
+    d = sc.dataset
+    data = occ.Data(d.x_train, d.y_train, d.x_val, d.y_val, d.x_test, d.y_test)
+    ref = {}
+    occ.coalition_value(data, [p.train_idx for p in sc.partners_list], [p.batch_size for p in sc.partners_list],
+                        coal, seed=eng.seed, epochs=eng.epoch_count, M=eng.minibatch_count, approach=approach,
+                        history=ref)
+    compare(res["history"], ref, coal)
+    assert eng.evaluate([coal])[0] == res["scores"][0]
