@@ -185,8 +185,11 @@ class Scenario:
         if self.coalition_values_file:
             self.load_coalition_values(self.coalition_values_file, missing_ok=True)
         # the main learning run records its history (mplc/mpl_utils.py:11-27), which the Federated SBS
-        # methods read (mplc/contributivity.py:1079-1115)
-        self.mpl = self.multi_partner_learning_approach(self, is_save_data=True, record_history=True)
+        # methods read (mplc/contributivity.py:1079-1115) - unless its value comes from a persisted table,
+        # whose point is to skip training (the history is then empty)
+        grand = tuple(range(self.partners_count))
+        record = grand not in getattr(self, "persisted_coalitions", ())
+        self.mpl = self.multi_partner_learning_approach(self, is_save_data=True, record_history=record)
         self.mpl.fit()
         if self.is_early_stopping or self.epoch_count <= constants.PATIENCE:  # same v(N) as Contributivity's
             self.coalition_values[tuple(range(self.partners_count))] = self.mpl.history.score
@@ -244,9 +247,13 @@ class Scenario:
         with np.load(path, allow_pickle=False) as f:
             if str(f["fingerprint"]) != self.coalition_values_fingerprint() or int(f["n"]) != self.partners_count:
                 raise ValueError(f"{path} was computed for another scenario configuration")
+            loaded = getattr(self, "persisted_coalitions", set())
             for m, v in zip(f["masks"], f["values"]):
                 m = int(m)
-                self.coalition_values[tuple(i for i in range(self.partners_count) if (m >> i) & 1)] = float(v)
+                key = tuple(i for i in range(self.partners_count) if (m >> i) & 1)
+                self.coalition_values[key] = float(v)
+                loaded.add(key)
+            self.persisted_coalitions = loaded
             return int(len(f["values"]))
 
     def append_contributivity(self, contributivity):
