@@ -197,13 +197,38 @@ __device__ int count_correct(const double* w, const float* X, const float* Y, in
   return (int)(block_sum(c, red) + 0.5);
 }
 
+__device__ int count_correct_rows(const double* w, const RowSel& rs, const float* X, const float* Y, int F,
+                                  double* red) {
+  double c = 0.0;
+  for (int i = threadIdx.x; i < rs.count; i += LR_THREADS) {
+    const int r = rs.row(i);
+    double z = w[F];
+    for (int k = 0; k < F; ++k) z += w[k] * (double)X[(int64_t)r * F + k];
+    c += ((z > 0.0) == (Y[r] > 0.5f)) ? 1.0 : 0.0;
+  }
+  return (int)(block_sum(c, red) + 0.5);
+}
+
+// Titanic.LogisticRegression.evaluate (mplc/dataset.py:343-351): [log_loss(y, predict(x)), accuracy] on hard
+// 0/1 predictions, from the count of correct predictions.  log_loss clips the 0/1 "probabilities" at the
+// machine epsilon of predict()'s dtype (sklearn's eps="auto", the version the reference runs with here and
+// that tests/golden/lr_history.json pins; sklearn 0.22 clipped at 1e-15): a partner model fitted on the
+// float32 labels predicts float32 classes (eps 2^-23), the aggregated model, built with int classes, float64
+// ones (eps 2^-52)
+constexpr double EPS_FITTED = 1.1920928955078125e-07, EPS_GLOBAL = 2.220446049250313e-16;
+__device__ void lr_metrics(int n_correct, int n, double& loss, double& acc, double eps) {
+  loss = ((double)(n - n_correct) * (-log(eps)) + (double)n_correct * (-log(1.0 - eps))) / (double)n;
+  acc = (double)n_correct / (double)n;
+}
+
 __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, int F, const int32_t* __restrict__ rows,
     const int32_t* __restrict__ rows_off, const int32_t* __restrict__ n_rows, const int32_t* __restrict__ splits,
     int M, const uint64_t* __restrict__ masks, const uint64_t* __restrict__ keys, const double* __restrict__ agg_w,
     const double* __restrict__ agg_scale, int epochs, int early_stopping, const float* __restrict__ Xv,
     const float* __restrict__ Yv, int n_val, const float* __restrict__ Xt, const float* __restrict__ Yt, int n_test,
-    int32_t* __restrict__ correct, int32_t* __restrict__ epochs_done, double* __restrict__ theta_out) {
+    int32_t* __restrict__ correct, int32_t* __restrict__ epochs_done, double* __restrict__ theta_out,
+    double* __restrict__ hist, int64_t hist_stride) {
   __shared__ Shared sh;
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
@@ -223,6 +248,15 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     newton_fit(rs, X, Y, F, sh);
     if (tid < D) theta_out[(int64_t)c * D + tid] = sh.w[tid];
     __syncthreads();
+    if (hist) {  // SinglePartnerLearning logs its fit at [0, 0]
+      const int ct = count_correct_rows(sh.w, rs, X, Y, F, sh.red);
+      const int cv = count_correct(sh.w, Xv, Yv, n_val, F, sh.red);
+      if (tid == 0) {
+        double* h = hist + (int64_t)c * hist_stride + 2;
+        lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
+        lr_metrics(cv, n_val, h[2], h[3], EPS_FITTED);
+      }
+    }
   } else {
     double* val_hist = sh.val_hist;
     int have = 0;  // the initial model is unfitted (coef_ None): evaluate -> [0, 0]
@@ -238,6 +272,14 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
         __syncthreads();
       }
       for (int m = 0; m < M; ++m) {
+        double* hrow = hist ? hist + (int64_t)c * hist_stride + (int64_t)(e * M + m) * (2 + 4 * LR_MAXP) : nullptr;
+        if (hrow) {  // the round-start collective model on val (eval_and_log_model_val_perf); unfitted: [0, 0]
+          const int cv = have ? count_correct(sh.theta, Xv, Yv, n_val, F, sh.red) : 0;
+          if (tid == 0) {
+            if (have) lr_metrics(cv, n_val, hrow[0], hrow[1], EPS_GLOBAL);
+            else hrow[0] = hrow[1] = 0.0;
+          }
+        }
         if (tid < D) sh.acc[tid] = 0.0;
         __syncthreads();
         for (int pi = 0; pi < P; ++pi) {
@@ -248,6 +290,15 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
           if (tid < D) sh.w[tid] = have ? sh.theta[tid] : 0.0;  // warm start from the global model
           __syncthreads();
           newton_fit(rs, X, Y, F, sh);
+          if (hrow) {  // the partner's fit history: [loss, accuracy] on its minibatch, then on val
+            const int ct = count_correct_rows(sh.w, rs, X, Y, F, sh.red);
+            const int cv = count_correct(sh.w, Xv, Yv, n_val, F, sh.red);
+            if (tid == 0) {
+              double* h = hrow + 2 + 4 * pi;
+              lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
+              lr_metrics(cv, n_val, h[2], h[3], EPS_FITTED);
+            }
+          }
           // np.average: multiply then sum in partner order (float64)
           if (tid < D) {
             const double prod = sh.w[tid] * agg_w[(int64_t)c * LR_MAXP + pi];
@@ -283,9 +334,11 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
                               const double* agg_scale, int n_coalitions, int epochs, int early_stopping,
                               const float* x_val, const float* y_val, int n_val, const float* x_test,
                               const float* y_test, int n_test, int32_t* correct, int32_t* epochs_done,
-                              double* theta_out, void* stream) {
+                              double* theta_out, double* hist, int64_t hist_stride, void* stream) {
   if (!x || !y || !rows || !rows_off || !n_rows || !splits || !masks || !keys || !agg_w || !agg_scale || !x_test ||
       !y_test || !correct || !epochs_done || !theta_out)
+    return MPLC_E_ARG;
+  if (hist && (!x_val || !y_val || n_val < 1 || hist_stride < (int64_t)epochs * minibatch_count * (2 + 4 * LR_MAXP)))
     return MPLC_E_ARG;
   // (D*D + D) Hessian+gradient entries must fit 4 per thread: D = n_features + 1 <= 31
   if (n_features < 1 || n_features + 1 > 31 || n_coalitions < 1 || minibatch_count < 1 || epochs < 1 ||
@@ -294,7 +347,8 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
   if (early_stopping && (!x_val || !y_val || n_val < 1)) return MPLC_E_ARG;
   lr_fedavg_kernel<<<n_coalitions, LR_THREADS, 0, (hipStream_t)stream>>>(
       x, y, n_features, rows, rows_off, n_rows, splits, minibatch_count, masks, keys, agg_w, agg_scale, epochs,
-      early_stopping, x_val, y_val, n_val, x_test, y_test, n_test, correct, epochs_done, theta_out);
+      early_stopping, x_val, y_val, n_val, x_test, y_test, n_test, correct, epochs_done, theta_out, hist,
+      hist_stride);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? MPLC_OK : (int)e;
 }

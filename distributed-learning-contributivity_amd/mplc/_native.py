@@ -48,7 +48,8 @@ SIGNATURES = {
     # batched FedAvg logistic regression (Titanic)
     "mplc_lr_fedavg": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
-                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                               c_void_p]),
 }
 
 ABI_VERSION = 1

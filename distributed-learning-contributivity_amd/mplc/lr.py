@@ -54,10 +54,18 @@ class LogRegEngine:
         self.profiler = None
         self.last_theta = None
 
-    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False):
+    supports_history = True
+    HIST_BLOCK = 2 + 4 * MAXP
+
+    def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
+                 record_history=False):
+        """v(S) for each coalition; with record_history (one coalition) the details also hold its learning
+        history (mplc/mpl_utils.py:11-27) in the layout of multi_partner_learning.History."""
         import torch
         coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
         C = len(coalitions)
+        if record_history and C != 1:
+            raise ValueError("record_history takes exactly one coalition")
         E = self.epoch_count if epoch_count is None else int(epoch_count)
         es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
         masks = np.zeros(C, dtype=np.uint64)
@@ -83,12 +91,20 @@ class LogRegEngine:
         correct = torch.zeros(C, dtype=torch.int32, device=dev)
         epochs_done = torch.zeros(C, dtype=torch.int32, device=dev)
         theta = torch.zeros((C, self.n_features + 1), dtype=torch.float64, device=dev)
+        M = self.minibatch_count
+        hist, stride = None, 0
+        if record_history:  # partner entries NaN, collective entries 0 until logged (History.__init__)
+            stride = E * M * self.HIST_BLOCK
+            h0 = np.zeros((E, M, self.HIST_BLOCK))
+            h0[:, :, 2:] = np.nan
+            hist = torch.from_numpy(h0.reshape(-1)).to(dev)
         P = _native.ptr
         st = _native.lib().mplc_lr_fedavg(
             P(self.x_train_d), P(self.y_train_d), self.n_features, P(self.rows_d), P(self.rows_off_d), P(self.n_rows_d),
             P(self.splits_d), self.minibatch_count, P(masks_d), P(keys_d), P(w_d), P(scale_d), C, E, 1 if es else 0,
             P(self.x_val_d), P(self.y_val_d), int(self.y_val_d.numel()), P(self.x_test_d), P(self.y_test_d),
-            int(self.y_test_d.numel()), P(correct), P(epochs_done), P(theta), _native.stream_handle(dev))
+            int(self.y_test_d.numel()), P(correct), P(epochs_done), P(theta),
+            P(hist) if hist is not None else None, stride, _native.stream_handle(dev))
         _native.check(st, "mplc_lr_fedavg")
         scores = correct.cpu().numpy().astype(np.float64) / float(self.y_test_d.numel())
         self.last_theta = theta.cpu().numpy()
@@ -96,5 +112,20 @@ class LogRegEngine:
         self.stats["batches"] += 1
         self.stats["replicas"] += sum(len(c) for c in coalitions)
         if return_details:
-            return {"scores": scores, "epochs_done": epochs_done.cpu().numpy().astype(np.int64)}
+            out = {"scores": scores, "epochs_done": epochs_done.cpu().numpy().astype(np.int64)}
+            if hist is not None:
+                out["history"] = self._history(coalitions[0], hist.cpu().numpy().reshape(E, M, self.HIST_BLOCK))
+            return out
         return scores
+
+    @staticmethod
+    def _history(coal, h):
+        names = ("loss", "accuracy", "val_loss", "val_accuracy")
+        out = {}
+        for pi, p in enumerate(coal):
+            out[p] = {k: np.ascontiguousarray(h[:, :, 2 + 4 * pi + i]) for i, k in enumerate(names)}
+            out[p] = {k: out[p][k] for k in ("val_accuracy", "val_loss", "loss", "accuracy")}
+        if len(coal) > 1:
+            out["mpl_model"] = {"val_accuracy": np.ascontiguousarray(h[:, :, 1]),
+                                "val_loss": np.ascontiguousarray(h[:, :, 0])}
+        return out

@@ -93,13 +93,20 @@ int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, cons
  *  keys[c*64 + i], agg_w[c*64 + i]: shuffle key and aggregation weight of the i-th partner (ascending id)
  *  of coalition c; agg_scale[c]: np.average's weight sum.  Outputs: correct[c] test hits,
  *  epochs_done[c], theta_out[c][n_features+1] = [coef | intercept].  n_features <= 30.
+ *  hist (NULL = off; needs x_val): the learning history (mplc/mpl_utils.py:11-27, logged by
+ *  mplc/multi_partner_learning.py:130-156) of coalition c at hist + c * hist_stride, round (e, m) at
+ *  offset (e*M + m) * (2 + 4*64): [collective val_loss, val_accuracy at the round start (0, 0 while
+ *  unfitted)] then per partner pi (ascending id) [loss, accuracy on its minibatch, val_loss,
+ *  val_accuracy] after its fit - Titanic.LogisticRegression.evaluate on hard predictions
+ *  (mplc/dataset.py:329-351).  A singleton writes its partner block of round (0, 0).  Unvisited entries
+ *  are left as the caller initialised them.  hist_stride >= epochs * M * (2 + 4 * 64).
  * ---------------------------------------------------------------------------------------------- */
 int mplc_lr_fedavg(const float* x, const float* y, int n_features, const int32_t* rows, const int32_t* rows_off,
                    const int32_t* n_rows, const int32_t* splits, int minibatch_count, const uint64_t* masks,
                    const uint64_t* keys, const double* agg_w, const double* agg_scale, int n_coalitions, int epochs,
                    int early_stopping, const float* x_val, const float* y_val, int n_val, const float* x_test,
                    const float* y_test, int n_test, int32_t* correct, int32_t* epochs_done, double* theta_out,
-                   void* stream);
+                   double* hist, int64_t hist_stride, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Monte-Carlo Shapley over a dense bitmask v(S) table (csrc/mc_shapley.hip).  V has 2^n fp64 entries,

@@ -17,6 +17,8 @@ Fixtures written (all data, no reference source):
   splits.json          - mplc/scenario.py:571-724 + mplc/dataset.py:62-106 partner index arrays and bs_p
   fedavg_lr.json       - mplc/multi_partner_learning.py:195-334 FedAvg with the Titanic LogisticRegression
                          model (mplc/dataset.py:323-394) on synthetic Titanic-shaped data: v(S) per coalition
+  lr_history.json      - mplc/mpl_utils.py:11-27 the learning history of the grand coalition's FedAvg fit on the
+                         fedavg_lr.json data
   sbs.json             - mplc/contributivity.py:1015-1115 Federated SBS linear / quadratic / constant on seeded
                          learning histories
 """
@@ -320,6 +322,55 @@ def gen_fedavg_lr(mplc):
 
 
 # --------------------------------------------------------------------------------------------------
+# (d2) learning history of the Titanic-LR FedAvg grand coalition (same data as gen_fedavg_lr)
+# --------------------------------------------------------------------------------------------------
+def gen_lr_history(mplc):
+    """mplc/mpl_utils.py:11-27 History.history of one FedAvg fit (is_early_stopping True, as Contributivity
+    builds it) of the grand coalition, per case of fedavg_lr.json (partition identical: same data, seed 42)."""
+    from sklearn.datasets import make_classification
+    from mplc.dataset import Dataset, Titanic
+
+    X, y = make_classification(n_samples=887, n_features=27, n_informative=8, random_state=0)
+    X = X.astype("float32")
+    y = y.astype("float32")
+    x_tr, x_te, y_tr, y_te = Titanic.train_test_split_global(X, y)
+
+    class SynthTitanic(Dataset):
+        train_test_split_local = staticmethod(Titanic.train_test_split_local)
+        train_val_split_local = staticmethod(Titanic.train_val_split_local)
+
+        def __init__(self):
+            super().__init__("titanic", (27,), 2, x_tr.copy(), y_tr.copy(), x_te.copy(), y_te.copy())
+
+        def generate_new_model(self):
+            clf = Titanic.LogisticRegression()
+            clf.classes_ = np.array([0, 1])
+            clf.metrics_names = ["log_loss", "Accuracy"]
+            return clf
+
+    out = []
+    for P, amounts, E, M in ((3, [0.2, 0.5, 0.3], 3, 1), (5, [0.2] * 5, 2, 1), (10, [0.1] * 10, 3, 1)):
+        ds = SynthTitanic()
+        sc = mplc.scenario.Scenario(P, amounts, dataset=ds, epoch_count=E, minibatch_count=M,
+                                    experiment_path=__import__("pathlib").Path("/tmp/mplc_golden_exp"))
+        sc.instantiate_scenario_partners()
+        sc.split_data(is_logging_enabled=False)
+        sc.compute_batch_sizes()
+        sc.save_folder = __import__("pathlib").Path("/tmp/mplc_golden_exp/save")
+        os.makedirs(sc.save_folder, exist_ok=True)
+        np.random.seed(0)
+        mpl = sc.multi_partner_learning_approach(sc, partners_list=np.array(sc.partners_list),
+                                                 is_early_stopping=True, is_save_data=False)
+        mpl.fit()
+        hist = {str(k): {m: np.asarray(v, dtype=float).tolist() for m, v in d.items()}
+                for k, d in mpl.history.history.items()}
+        out.append({"partners_count": P, "epoch_count": E, "minibatch_count": M, "score": float(mpl.history.score),
+                    "history": hist})
+        print(f"lr history P={P}", flush=True)
+    return out
+
+
+# --------------------------------------------------------------------------------------------------
 # (e) Federated step-by-step scores on synthetic learning histories
 # --------------------------------------------------------------------------------------------------
 def gen_sbs(mplc):
@@ -362,7 +413,7 @@ def main():
     only = set(sys.argv[1:])
     mplc = import_reference()
     jobs = {"shapley_value": gen_shapley, "estimators": gen_estimators, "splits": gen_splits,
-            "fedavg_lr": gen_fedavg_lr, "sbs": gen_sbs}
+            "fedavg_lr": gen_fedavg_lr, "sbs": gen_sbs, "lr_history": gen_lr_history}
     for name, fn in jobs.items():
         if only and name not in only:
             continue

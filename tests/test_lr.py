@@ -109,3 +109,60 @@ def test_titanic_exact_shapley_all_1023_coalitions():
     c.compute_contributivity("Shapley values")
     assert c.first_charac_fct_calls_count == 1023
     assert abs(np.sum(c.contributivity_scores) - c.charac_fct_values[tuple(range(10))]) < 1e-12
+
+
+@pytest.mark.gpu
+def test_lr_history_matches_reference(golden):
+    """The grand coalition's learning history (mplc/mpl_utils.py:11-27) against the reference's own
+    (tests/golden/lr_history.json: FederatedAverageLearning with Titanic.LogisticRegression on the same
+    data and partition).  Accuracies are counts over val / minibatch rows: equal, or one sample apart where
+    lbfgs' tolerance moves a point across the boundary; losses are those counts through log_loss."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "lr_history.json")) as f:
+        hcases = json.load(f)["data"]
+    from mplc.engine import CoalitionEngine
+    exact, total = 0, 0
+    for case, hc in zip(golden["cases"], hcases):
+        assert hc["partners_count"] == case["partners_count"]
+        sc = scenario_for(golden, case)
+        eng = CoalitionEngine.for_scenario(sc)
+        n = case["partners_count"]
+        res = eng.evaluate([tuple(range(n))], return_details=True, record_history=True)
+        h = res["history"]
+        ref = {(k if k == "mpl_model" else int(k)): v for k, v in hc["history"].items()}
+        assert set(h) == set(ref)
+        n_val = len(sc.dataset.y_val)
+        for k, metrics in ref.items():
+            for m, r in metrics.items():
+                r = np.asarray(r, dtype=float)
+                d = h[k][m]
+                assert d.shape == r.shape
+                if m.endswith("accuracy"):
+                    rows = n_val if m == "val_accuracy" else len(sc.partners_list[k].y_train)
+                    assert np.all(np.abs(d - r) * rows <= 1 + 1e-9), (k, m, d, r)
+                    total += d.size
+                    exact += int(np.sum(d == r))
+        for k in ref:  # loss = f(accuracy): equal wherever the accuracy is
+            for m in ("val_loss",) + (("loss",) if k != "mpl_model" else ()):
+                acc = "val_accuracy" if m == "val_loss" else "accuracy"
+                same = h[k][acc] == np.asarray(ref[k][acc])
+                np.testing.assert_allclose(h[k][m][same], np.asarray(ref[k][m])[same], rtol=1e-9)
+    assert exact >= 0.9 * total
+
+
+@pytest.mark.gpu
+def test_titanic_scenario_run_records_history_and_federated_sbs(golden):
+    sc = scenario_for(golden, golden["cases"][1])
+    sc.methods = ["Federated SBS linear", "Federated SBS constant"]
+    sc.run()
+    hist = sc.mpl.history.history
+    assert set(hist) == set(range(5)) | {"mpl_model"}
+    assert hist["mpl_model"]["val_accuracy"][0, 0] == 0.0  # the unfitted initial model evaluates to [0, 0]
+    lin, const = sc.contributivity_list
+    # E*M = 2 rounds: the kept rounds include round 0, whose collective model is the unfitted one (accuracy
+    # 0), so the relative performances are inf there - the reference's own arithmetic, reproduced
+    E, M = 2, 1
+    rel = np.stack([hist[p]["val_accuracy"] for p in range(5)], axis=-1).reshape(E * M, 5)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rel = (rel / hist["mpl_model"]["val_accuracy"].reshape(E * M)[:, None])[0:2]
+        np.testing.assert_array_equal(const.contributivity_scores, np.nanmean(rel, axis=0))
+    assert np.all(np.isinf(const.contributivity_scores))
