@@ -76,6 +76,11 @@ class Scenario:
         except KeyError:
             raise KeyError(f"Multi-partner learning approach '{multi_partner_learning_approach}' is not a valid "
                            f"approach. List of supported approach : {', '.join(MULTI_PARTNER_LEARNING_APPROACHES)}, ")
+        if aggregation_weighting == "local-score":
+            # registered in the reference (mplc/mpl_utils.py:132-136) but its aggregate_model_weights returns
+            # None (:118-128), so the next round's models are None: rejected here instead of failing mid-run
+            raise NotImplementedError("'local-score' aggregation is broken in the reference (its aggregator "
+                                      "returns no weights); use 'data-volume' or 'uniform' (DESIGN.md)")
         if aggregation_weighting not in AGGREGATION_SCHEMES:
             raise ValueError(f"aggregation approach '{aggregation_weighting}' is not a valid approach. ")
         self.aggregation_weighting = aggregation_weighting

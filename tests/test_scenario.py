@@ -83,6 +83,18 @@ def test_aggregation_weights_match_reference_aggregators():
     assert wu == [1 / 3] * 3
 
 
+def test_local_score_aggregation_is_rejected():
+    """'local-score' is registered in the reference (mplc/mpl_utils.py:132-136) but its aggregator returns
+    no weights (:118-128); the scenario refuses it up front."""
+    import pytest
+    from mplc.dataset import ArrayDataset, digits_as_mnist
+    from mplc.scenario import Scenario
+    x, y = digits_as_mnist()
+    ds = ArrayDataset(x[:600], y[:600], x[600:800], y[600:800], name="mnist")
+    with pytest.raises(NotImplementedError, match="local-score"):
+        Scenario(2, [0.5, 0.5], dataset=ds, aggregation_weighting="local-score")
+
+
 def test_host_and_oracle_keys_agree():
     for s in (0, 1, 12345):
         for mask in (1, 3, 1023, 0x3FF):
