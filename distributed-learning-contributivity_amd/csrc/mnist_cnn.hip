@@ -138,19 +138,28 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv1 (recompute) + conv2 (MFMA) + bias + ReLU + 2x2 max-pool.  Block = (half image, slot, model).
-// 9 tiles x 2 channel tiles of 32x32; a tile = 8 pooling windows x 4 pixels, laid out so that the 4
-// pixels of a window are accumulator registers 4g..4g+3 of one lane: the pool is a register max.
+// conv1 (recompute) + conv2 (MFMA) + bias + ReLU + 2x2 max-pool.  Block = (third of the image: 4 pool rows,
+// slot, model), 4 waves - one per SIMD, so the block's MFMA work is spread evenly over the CU.  6 row tiles
+// x 2 channel tiles of 32x32; wave w owns channel tile w & 1 of row tiles 3 (w >> 1) .. +2.  A row tile =
+// 8 pooling windows x 4 pixels, laid out so that the 4 pixels of a window are accumulator registers
+// 4g..4g+3 of one lane: the pool is a register max.  A third needs 10 conv1 rows (34 KB of LDS): four
+// blocks share a CU.
 // ------------------------------------------------------------------------------------------------
-constexpr int FWD_THREADS = 192;
+constexpr int FWD_THREADS = 256;
+constexpr int FWD_PR = 4;                          // pool rows per block
+constexpr int FWD_PARTS = PL / FWD_PR;             // blocks per image
+constexpr int FWD_C1R = 2 * FWD_PR + 2;            // conv1 rows per block
+constexpr int FWD_IMR = FWD_C1R + 2;               // image rows per block
+constexpr int FWD_C1T = (FWD_C1R * A1 + 31) / 32;  // conv1 tiles (9)
+static_assert(FWD_PR * PL / 8 == 6, "6 row tiles per block: 2 wave groups x 3");
 
-__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_fwd_kernel(
+__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, float* __restrict__ pooled,
     uint8_t* __restrict__ code) {
-  __shared__ float img_s[16 * IMG];
-  __shared__ float a1_s[14 * A1 * A1P];
-  const int half = blockIdx.x;
+  __shared__ float img_s[FWD_IMR * IMG];
+  __shared__ float a1_s[FWD_C1R * A1 * A1P];
+  const int part = blockIdx.x;
   const int j = blockIdx.y;
   const int r = blockIdx.z;
   const int count = cnt ? cnt[r] : cnt_all;
@@ -158,37 +167,40 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   const int tid = threadIdx.x;
   const int row = idx ? idx[(int64_t)r * bmax + j] : row_base + j;
   const float* P = params + (int64_t)r * stride;
-  const float* xi = x + (int64_t)row * (IMG * IMG) + half * 12 * IMG;
+  const float* xi = x + (int64_t)row * (IMG * IMG) + part * 2 * FWD_PR * IMG;
   {  // all of the block's image loads in flight at once
-    constexpr int NIT = (16 * IMG + FWD_THREADS - 1) / FWD_THREADS;
+    constexpr int NIT = (FWD_IMR * IMG + FWD_THREADS - 1) / FWD_THREADS;
     float v[NIT];
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
       const int e = tid + FWD_THREADS * k;
-      v[k] = xi[e < 16 * IMG ? e : 0];
+      v[k] = xi[e < FWD_IMR * IMG ? e : 0];
     }
 #pragma unroll
     for (int k = 0; k < NIT; ++k)
-      if (tid + FWD_THREADS * k < 16 * IMG) img_s[tid + FWD_THREADS * k] = v[k];
+      if (tid + FWD_THREADS * k < FWD_IMR * IMG) img_s[tid + FWD_THREADS * k] = v[k];
   }
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
+  const int nt = wave & 1, tg = wave >> 1;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
   __syncthreads();
-  // conv1 + ReLU for local rows 0..13 (global 12*half + lr): 364 positions = 12 MFMA tiles, 4 per wave
-  constexpr int NPOS1 = 14 * A1;
+  // conv1 + ReLU for local rows 0..FWD_C1R-1 (global 2*FWD_PR*part + lr): FWD_C1T MFMA tiles over 4 waves
+  constexpr int NPOS1 = FWD_C1R * A1;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int t = wave + 3 * u;
-    const int p = min(t * 32 + m, NPOS1 - 1);
-    const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
+  for (int u = 0; u < (FWD_C1T + 3) / 4; ++u) {
+    const int t = wave + 4 * u;
+    if (t < FWD_C1T) {  // wave-uniform
+      const int p = min(t * 32 + m, NPOS1 - 1);
+      const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int pw = t * 32 + acc_row(reg, kh);
-      if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
+      for (int reg = 0; reg < 16; ++reg) {
+        const int pw = t * 32 + acc_row(reg, kh);
+        if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
+      }
     }
   }
   __syncthreads();
@@ -196,27 +208,24 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   int pbase[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    const int t = wave + 3 * u;
+    const int t = 3 * tg + u;
     const int wi = 8 * t + (m >> 2);
     const int pr = wi / PL, pc = wi % PL;
     const int q = m & 3;
     const int oy = 2 * pr + (q >> 1), ox = 2 * pc + (q & 1);
     pbase[u] = (oy * A1 + ox) * A1P;
   }
-  floatx16 acc[3][2];
+  floatx16 acc[3];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
-  // K = 9 taps x 32 channels in 18 groups of 8 channel pairs; the B operand (W2, L2-resident) of group g + 1
-  // is loaded into registers while group g's 48 MFMAs run
-  const float* W2 = P + OFF_W2 + kh * C2 + m;
-  float bcur[16], bnxt[16];
-  auto load_b = [&](int g, float (&b)[16]) {
+  for (int u = 0; u < 3; ++u) acc[u] = zero16();
+  // K = 9 taps x 32 channels in 18 groups of 8 channel pairs; the B operand (this wave's 32 columns of W2,
+  // L2-resident) of group g + 1 is loaded into registers while group g's MFMAs run
+  const float* W2 = P + OFF_W2 + kh * C2 + nt * 32 + m;
+  float bcur[8], bnxt[8];
+  auto load_b = [&](int g, float (&b)[8]) {
     const float* w = W2 + (int64_t)((g >> 1) * C1 + (g & 1) * 16) * C2;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      b[2 * i] = w[2 * i * C2];
-      b[2 * i + 1] = w[2 * i * C2 + 32];
-    }
+    for (int i = 0; i < 8; ++i) b[i] = w[2 * i * C2];
   };
   load_b(0, bcur);
 #pragma unroll
@@ -227,40 +236,33 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const float a = a1_s[pbase[u] + off + 2 * i];
-        acc[u][0] = mfma32(a, bcur[2 * i], acc[u][0]);
-        acc[u][1] = mfma32(a, bcur[2 * i + 1], acc[u][1]);
-      }
+      for (int u = 0; u < 3; ++u) acc[u] = mfma32(a1_s[pbase[u] + off + 2 * i], bcur[i], acc[u]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bcur[i] = bnxt[i];
+    for (int i = 0; i < 8; ++i) bcur[i] = bnxt[i];
   }
   // epilogue: bias, ReLU, 2x2 max-pool (first max in window scan order), argmax code
   float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
   uint8_t* outc = code ? code + ((int64_t)r * bmax + j) * FEAT : nullptr;
+  const int co = nt * 32 + m;
+  const float bias = P[OFF_B2 + co];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    const int t = wave + 3 * u;
+    const int t = 3 * tg + u;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int co = nt * 32 + m;
-      const float bias = P[OFF_B2 + co];
+    for (int g = 0; g < 4; ++g) {
+      const int wi = 8 * t + 2 * g + kh;
+      const int py = FWD_PR * part + wi / PL, px = wi % PL;
+      float best = acc[u][4 * g] + bias;
+      int arg = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int wi = 8 * t + 2 * g + kh;
-        const int py = 6 * half + wi / PL, px = wi % PL;
-        float best = acc[u][nt][4 * g] + bias;
-        int arg = 0;
-#pragma unroll
-        for (int qq = 1; qq < 4; ++qq) {
-          const float z = acc[u][nt][4 * g + qq] + bias;
-          if (z > best) { best = z; arg = qq; }
-        }
-        const int pidx = (py * PL + px) * C2 + co;
-        outp[pidx] = fmaxf(best, 0.0f);
-        if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
+      for (int qq = 1; qq < 4; ++qq) {
+        const float z = acc[u][4 * g + qq] + bias;
+        if (z > best) { best = z; arg = qq; }
       }
+      const int pidx = (py * PL + px) * C2 + co;
+      outp[pidx] = fmaxf(best, 0.0f);
+      if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
     }
   }
 }
@@ -1027,7 +1029,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t);
   PROF_BEGIN(1);
-  conv_fwd_kernel<<<dim3(2, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->pooled,
+  conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->pooled,
                                                          t->code);
   PROF_END(1);
   PROF_BEGIN(2);
@@ -1069,7 +1071,7 @@ int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const f
   hipStream_t s = (hipStream_t)stream;
   for (int s0 = 0; s0 < n_samples; s0 += chunk) {
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
-    conv_fwd_kernel<<<dim3(2, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
+    conv_fwd_kernel<<<dim3(FWD_PARTS, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
                                                                   pooled, nullptr);
     dense_fwd_kernel<<<dim3((cn + 31) / 32, n_models), 256, 0, s>>>(pooled, (int64_t)chunk * FEAT, nullptr, cn, chunk,
                                                                     params, stride, hidden);
