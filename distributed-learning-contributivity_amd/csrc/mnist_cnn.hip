@@ -767,24 +767,54 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
 
 // ------------------------------------------------------------------------------------------------
 // conv2 weight gradient: dW2[kyx*32+ci][co] = sum_px a1[py+ky][px+kx][ci] dZ2[px][co]; db2.
-// Block = (split s, replica r): samples [8s, 8s+8); 3 waves, wave w owns rows ky = w (kx = 0..2) x 64 co.
+// Block = (split s, replica r): samples [8s, 8s+8); 4 waves (one per SIMD), the 288 x 64 output split by
+// area: wave w owns rows [144*(w>>1), +144) (9 tiles of 16 = (kyx, ci half)) x cols [32*(w&1), +32) on
+// v_mfma_f32_16x16x4_f32 (72 accumulator registers).  Per k-step of 4 pixels a wave reads 9 A and 2 B
+// operands for 18 MFMAs.  Both operands are staged in LDS as [half|quarter][pixel][16] planes, so every
+// ds_read_b32 is one contiguous 64-lane run (conflict-free) and the lane offset is the lane id.
 // Per band of 4 conv2 rows: conv1 rows recomputed on MFMA (conv1_mfma) into LDS, dZ2 un-pooled from the
 // prefetched (dp, code) registers; the K loop over the band's 96 pixels is fully unrolled (compile-time
 // LDS offsets).  The next band's (dp, code) are fetched while the current band's MFMAs run.
+// Each output element is still one k-ordered f32 FMA chain over the split's pixels (sample, band, pixel).
 // ------------------------------------------------------------------------------------------------
-constexpr int WG_THREADS = 192;
-constexpr int WG_SAMPLES = 8;  // samples per wgrad split (fixed: reproducible sums)
-constexpr int WGP = 65;        // padded channel stride of the dense dZ2 band
-constexpr int WG_PRE = 8;      // pooled pairs per thread per band: 2 rows x 12 x 64 / 192
+constexpr int WG_THREADS = 256;
+constexpr int WG_SAMPLES = 8;             // samples per wgrad split (fixed: reproducible sums)
+constexpr int WG_PRE = 6;                 // pooled pairs per thread per band: 2 rows x 12 x 64 / 256
+constexpr int WG_A1H = 6 * A1 * 16 + 16;  // one ci-half plane of the band's conv1 rows (+16: write banks)
+constexpr int WG_DZQ = 4 * Z2 * 16 + 16;  // one co-quarter plane of the band's dense dZ2 (+16: write banks)
+
+__device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// K loop over one band's 96 conv2 pixels, four per MFMA (px = 4*s4 + (lane >> 4)), for row half RH
+// (compile-time, so every LDS offset is an immediate).
+template <int RH>
+__device__ __forceinline__ void wgrad_band(const float* abase, const float* zb, fvec4 (&acc)[9][2]) {
+#pragma unroll
+  for (int s4 = 0; s4 < 24; ++s4) {
+    const int oyl = (4 * s4) / Z2, ox0 = (4 * s4) % Z2;
+    const float b0 = zb[(oyl * Z2 + ox0) * 16];
+    const float b1 = zb[WG_DZQ + (oyl * Z2 + ox0) * 16];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int t = 9 * RH + i;  // 16-row tile: kyx = t >> 1, ci half t & 1
+      const int kyx = t >> 1;
+      const float a = abase[(t & 1) * WG_A1H + ((oyl + kyx / 3) * A1 + ox0 + kyx % 3) * 16];
+      acc[i][0] = mfma16(a, b0, acc[i][0]);
+      acc[i][1] = mfma16(a, b1, acc[i][1]);
+    }
+  }
+}
 
 __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
   __shared__ float img_s[IMG * IMG];
-  __shared__ float a1_s[6 * A1 * C1];
-  __shared__ float dzd_s[4 * Z2 * WGP];  // dense un-pooled dZ2 of the band: [4 rows][24 cols][65]
-  __shared__ float gb_s[3][C2];
+  __shared__ float a1_s[2 * WG_A1H];
+  __shared__ float dzd_s[4 * WG_DZQ];
+  __shared__ float gb_s[4][C2];
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -797,16 +827,21 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const int lane = tid & 63, wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
+  const int rh = wave >> 1;  // row half: 16-row tiles 9*rh .. 9*rh+8
+  const int ch = wave & 1;   // col half: co quarters 2*ch, 2*ch+1
   const float* P = params + (int64_t)r * stride;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
-  floatx16 acc[3][2];
+  fvec4 acc[9][2];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) { acc[u][0] = zero16(); acc[u][1] = zero16(); }
+  for (int i = 0; i < 9; ++i) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[i][c] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  }
   float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread un-pools has that channel)
   float pdv[WG_PRE];
   uint32_t pcd[WG_PRE];
-  // pooled rows 2*band, 2*band+1 of sample jj: pair e = tid + 192*s is element 24*64*band + e (contiguous)
+  // pooled rows 2*band, 2*band+1 of sample jj: pair e = tid + 256*s is element 24*64*band + e (contiguous)
   auto fetch = [&](int jj, int band) {
     const int64_t base = ((int64_t)r * bmax + jj) * FEAT + band * 2 * PL * C2;
 #pragma unroll
@@ -829,11 +864,9 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   };
   fetch(j_begin, 0);
   fetch_img(j_begin);
-  // A-operand bases: row tile u = (ky = wave, kx = u) x 32 ci, lane (kh, m) reads pixel px0 + kh, channel m
-  const int zb = kh * WGP + m;
-  int ab[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u) ab[u] = (wave * A1 + u) * C1 + kh * C1 + m;
+  // operand planes: lane l reads pixel (k-step base + (l >> 4)), row/col (l & 15) -> plane offset l
+  const float* zb = dzd_s + (2 * ch) * WG_DZQ + lane;
+  const float* abase = a1_s + lane;
   for (int j = j_begin; j < j_end; ++j) {
 #pragma unroll
     for (int k = 0; k < IMG_PRE; ++k)
@@ -850,21 +883,22 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const float v = (c & 0x80) ? pdv[s] : 0.0f;
         gb += v;
         const int sel = c & 3;
+        float* d = dzd_s + (co >> 4) * WG_DZQ + (co & 15);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          dzd_s[((2 * prr + (q >> 1)) * Z2 + 2 * pc + (q & 1)) * WGP + co] = (sel == q) ? v : 0.0f;
+        for (int q = 0; q < 4; ++q) d[((2 * prr + (q >> 1)) * Z2 + 2 * pc + (q & 1)) * 16] = (sel == q) ? v : 0.0f;
       }
-      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles (waves 0,1: two; wave 2: one)
+      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles (wave 0: two; waves 1-3: one)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int t = wave + 3 * u;
+        const int t = wave + 4 * u;
         if (t < 5) {
           const int p = min(t * 32 + m, 6 * A1 - 1);
           const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
+          float* dst = a1_s + (m >> 4) * WG_A1H + (m & 15);
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) {
             const int pw = t * 32 + acc_row(reg, kh);
-            if (pw < 6 * A1) a1_s[pw * C1 + m] = fmaxf(a[reg], 0.0f);
+            if (pw < 6 * A1) dst[pw * 16] = fmaxf(a[reg], 0.0f);
           }
         }
       }
@@ -875,38 +909,24 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         fetch_img(j + 1);
       }
       __syncthreads();
-      // K loop over the band's 96 conv2 pixels, two per MFMA (lane half kh): px = 2*s2 + kh
-#pragma unroll
-      for (int s2 = 0; s2 < 48; ++s2) {
-        const int oyl = (2 * s2) / Z2, ox0 = (2 * s2) % Z2;
-        const float bz0 = dzd_s[zb + (oyl * Z2 + ox0) * WGP];
-        const float bz1 = dzd_s[zb + (oyl * Z2 + ox0) * WGP + 32];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const float a = a1_s[ab[u] + (oyl * A1 + ox0) * C1];
-          acc[u][0] = mfma32(a, bz0, acc[u][0]);
-          acc[u][1] = mfma32(a, bz1, acc[u][1]);
-        }
-      }
+      if (rh == 0) wgrad_band<0>(abase, zb, acc);
+      else wgrad_band<1>(abase, zb, acc);
     }
     __syncthreads();  // last band's readers done before the next sample's img_s load
   }
   float* out = w2_part + ((int64_t)r * splits + sp) * MPLC_CNN_W2P;
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int kyx = 3 * wave + u;
+  for (int i = 0; i < 9; ++i) {
+    const int row0 = 16 * (9 * rh + i) + 4 * (lane >> 4);  // row = kyx*32 + ci
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int c = 0; c < 2; ++c) {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int ci = acc_row(reg, kh);
-        out[(kyx * C1 + ci) * C2 + nt * 32 + m] = acc[u][nt][reg];
-      }
+      for (int rr = 0; rr < 4; ++rr) out[(row0 + rr) * C2 + 32 * ch + 16 * c + (lane & 15)] = acc[i][c][rr];
     }
   }
   gb_s[wave][lane] = gb;
   __syncthreads();
-  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + gb_s[2][tid];
+  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + (gb_s[2][tid] + gb_s[3][tid]);
 }
 
 // Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
