@@ -777,9 +777,11 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
 // LDS offsets).  The next band's (dp, code) are fetched while the current band's MFMAs run.
 // Each output element is still one k-ordered f32 FMA chain over the split's pixels (sample, band, pixel).
 // ------------------------------------------------------------------------------------------------
-constexpr int WG_THREADS = 256;
+constexpr int WG_NC = 2;                  // 16-col tiles per wave (4 / WG_NC waves per row half)
+constexpr int WG_WAVES = 8 / WG_NC;
+constexpr int WG_THREADS = 64 * WG_WAVES;
 constexpr int WG_SAMPLES = 8;             // samples per wgrad split (fixed: reproducible sums)
-constexpr int WG_PRE = 6;                 // pooled pairs per thread per band: 2 rows x 12 x 64 / 256
+constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // pooled pairs per thread per band: 2 rows x 12 x 64
 constexpr int WG_A1H = 6 * A1 * 16 + 16;  // one ci-half plane of the band's conv1 rows (+16: write banks)
 constexpr int WG_DZQ = 4 * Z2 * 16 + 16;  // one co-quarter plane of the band's dense dZ2 (+16: write banks)
 
@@ -790,31 +792,32 @@ __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
 // K loop over one band's 96 conv2 pixels, four per MFMA (px = 4*s4 + (lane >> 4)), for row half RH
 // (compile-time, so every LDS offset is an immediate).
 template <int RH>
-__device__ __forceinline__ void wgrad_band(const float* abase, const float* zb, fvec4 (&acc)[9][2]) {
+__device__ __forceinline__ void wgrad_band(const float* abase, const float* zb, fvec4 (&acc)[9][WG_NC]) {
 #pragma unroll
   for (int s4 = 0; s4 < 24; ++s4) {
     const int oyl = (4 * s4) / Z2, ox0 = (4 * s4) % Z2;
-    const float b0 = zb[(oyl * Z2 + ox0) * 16];
-    const float b1 = zb[WG_DZQ + (oyl * Z2 + ox0) * 16];
+    float b[WG_NC];
+#pragma unroll
+    for (int c = 0; c < WG_NC; ++c) b[c] = zb[c * WG_DZQ + (oyl * Z2 + ox0) * 16];
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int t = 9 * RH + i;  // 16-row tile: kyx = t >> 1, ci half t & 1
       const int kyx = t >> 1;
       const float a = abase[(t & 1) * WG_A1H + ((oyl + kyx / 3) * A1 + ox0 + kyx % 3) * 16];
-      acc[i][0] = mfma16(a, b0, acc[i][0]);
-      acc[i][1] = mfma16(a, b1, acc[i][1]);
+#pragma unroll
+      for (int c = 0; c < WG_NC; ++c) acc[i][c] = mfma16(a, b[c], acc[i][c]);
     }
   }
 }
 
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(WG_WAVES / 2, WG_WAVES / 2))) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
   __shared__ float img_s[IMG * IMG];
   __shared__ float a1_s[2 * WG_A1H];
   __shared__ float dzd_s[4 * WG_DZQ];
-  __shared__ float gb_s[4][C2];
+  __shared__ float gb_s[WG_WAVES][C2];
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -827,16 +830,16 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const int lane = tid & 63, wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
-  const int rh = wave >> 1;  // row half: 16-row tiles 9*rh .. 9*rh+8
-  const int ch = wave & 1;   // col half: co quarters 2*ch, 2*ch+1
+  const int rh = wave / (4 / WG_NC);  // row half: 16-row tiles 9*rh .. 9*rh+8
+  const int ch = wave % (4 / WG_NC);  // col group: co quarters WG_NC*ch .. +WG_NC-1
   const float* P = params + (int64_t)r * stride;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
-  fvec4 acc[9][2];
+  fvec4 acc[9][WG_NC];
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) acc[i][c] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int c = 0; c < WG_NC; ++c) acc[i][c] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   }
   float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread un-pools has that channel)
   float pdv[WG_PRE];
@@ -865,7 +868,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   fetch(j_begin, 0);
   fetch_img(j_begin);
   // operand planes: lane l reads pixel (k-step base + (l >> 4)), row/col (l & 15) -> plane offset l
-  const float* zb = dzd_s + (2 * ch) * WG_DZQ + lane;
+  const float* zb = dzd_s + (WG_NC * ch) * WG_DZQ + lane;
   const float* abase = a1_s + lane;
   for (int j = j_begin; j < j_end; ++j) {
 #pragma unroll
@@ -887,10 +890,10 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
         for (int q = 0; q < 4; ++q) d[((2 * prr + (q >> 1)) * Z2 + 2 * pc + (q & 1)) * 16] = (sel == q) ? v : 0.0f;
       }
-      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles (wave 0: two; waves 1-3: one)
+      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles of 32 over the block's waves
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = wave + 4 * u;
+      for (int u = 0; u < (5 + WG_WAVES - 1) / WG_WAVES; ++u) {
+        const int t = wave + WG_WAVES * u;
         if (t < 5) {
           const int p = min(t * 32 + m, 6 * A1 - 1);
           const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
@@ -919,14 +922,19 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   for (int i = 0; i < 9; ++i) {
     const int row0 = 16 * (9 * rh + i) + 4 * (lane >> 4);  // row = kyx*32 + ci
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < WG_NC; ++c) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) out[(row0 + rr) * C2 + 32 * ch + 16 * c + (lane & 15)] = acc[i][c][rr];
+      for (int rr = 0; rr < 4; ++rr) out[(row0 + rr) * C2 + 16 * (WG_NC * ch + c) + (lane & 15)] = acc[i][c][rr];
     }
   }
   gb_s[wave][lane] = gb;
   __syncthreads();
-  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + (gb_s[2][tid] + gb_s[3][tid]);
+  if (tid < C2) {
+    float g = 0.0f;
+#pragma unroll
+    for (int w = 0; w < WG_WAVES; ++w) g += gb_s[w][tid];
+    out[9 * C1 * C2 + tid] = g;
+  }
 }
 
 // Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
