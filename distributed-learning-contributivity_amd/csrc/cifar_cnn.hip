@@ -471,8 +471,9 @@ struct WgArgs {
   int off_w, off_b;
 };
 
-template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BR, int NW>
-__global__ __launch_bounds__(NW * 64) void wgrad_kernel(const WgArgs a) {
+template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BR, int NW, int WPE = 0>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, WPE > 0 ? WPE : 8)))
+void wgrad_kernel(const WgArgs a) {
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr int WOE = WOV + (WOV & 1);
   constexpr int WXP = WI + 2 * PAD + 1;
@@ -1066,9 +1067,9 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 16, 4, 2, EPI_BWD_UNPOOL, 2> /* 1 band, 42.0 KB */
 #define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 16, 4, 4, EPI_BWD_MASK, 2> /* 2 bands, 42.0 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
-#define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 5, 3>
+#define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 3, 3>
 #define CONV3_WGRAD wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 5, 3>
-#define CONV4_WGRAD wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 6>
+#define CONV4_WGRAD wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 6, 3>
 
 inline int launch_status() {
   const hipError_t e = hipGetLastError();
