@@ -15,7 +15,7 @@ from . import _native
 
 STRIDE = 1251008
 NPARAM = 1250954
-WG_SAMPLES = 4
+WG_SAMPLES = 2
 A1, D2, A3, D4, H5 = 32768, 7200, 14400, 2304, 512
 DZ4, DZ3, DZ2, DZ1 = 10816, 14400, 28800, 32768
 WT, WPART = 64512, 65664

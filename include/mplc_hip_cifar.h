@@ -60,7 +60,7 @@ extern "C" {
 #define MPLC_CIFAR_DZ1 32768         /* conv1 pre-activation gradient 32x32x32    */
 #define MPLC_CIFAR_WT 64512          /* flipped/transposed W2|W3|W4 for the data gradients */
 #define MPLC_CIFAR_WPART 65664       /* partial gradient row of W1..b4 (= params layout prefix) */
-#define MPLC_CIFAR_WG_SAMPLES 4      /* samples per weight-gradient split (fixed: reproducible sums) */
+#define MPLC_CIFAR_WG_SAMPLES 2      /* samples per weight-gradient split (fixed: reproducible sums) */
 
 typedef struct {
   /* geometry */
