@@ -71,6 +71,17 @@ __device__ __forceinline__ bool drop_keep(uint32_t row_seed, uint32_t e, uint32_
   return (hash32(row_seed ^ e) >> 8) >= thr;
 }
 
+// Cross-lane add within rows of 16 lanes on DPP (VALU, no LDS round trip).  Each level adds the partner's
+// value exactly as `d += __shfl_xor(d, m)` does (commutative adds of the same operands: bit-identical).
+template <int CTRL>
+__device__ __forceinline__ float dpp_partner(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141;  // lane i <-> 7 - i within 8 (the other quad after two levels)
+constexpr int DPP_MIRROR = 0x140;       // lane i <-> 15 - i within 16 (the other 8 after three levels)
+
 __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -958,10 +969,10 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
           g[i].x += pv * dh.x; g[i].y += pv * dh.y; g[i].z += pv * dh.z; g[i].w += pv * dh.w;
           d += dh.x * w[i].x; d += dh.y * w[i].y; d += dh.z * w[i].z; d += dh.w * w[i].w;
         }
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        d += __shfl_xor(d, 8, 64);
+        d += dpp_partner<DPP_XOR1>(d);
+        d += dpp_partner<DPP_XOR2>(d);
+        d += dpp_partner<DPP_HALF_MIRROR>(d);
+        d += dpp_partner<DPP_MIRROR>(d);
         d += __shfl_xor(d, 16, 64);
         if (c32 < 4) {  // un-pool: lane c32 = q writes window pixel q
           const uint32_t c = c_s[jj * KB + grp * D5_ROWS + rowl];
