@@ -64,41 +64,67 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-// Weight tables in LDS: cw[s] = w(s-1) + w(s), bw[s] = w(s), s = 0..n (zero beyond).
-__device__ __forceinline__ void build_weights(int n, double* cw, double* bw) {
+// Weight tables cw[s] = w(s-1) + w(s), bw[s] = w(s), s = 0..n (zero beyond), computed once on the host (IEEE
+// fp64, the same operation order for every launch) and passed by value as a kernel argument: a block copies
+// them into LDS instead of re-deriving the binomials with fp64 divisions (that prologue used to cost more
+// than the 512 KiB a block streams at n = 24).
+struct Weights {
+  double cw[MAX_N + 2];
+  double bw[MAX_N + 2];
+};
+
+inline double weight_w(int n, int s) {  // w(s) = 1 / (n C(n-1, s)), 0 outside [0, n-1]
+  if (s < 0 || s >= n) return 0.0;
+  double C = 1.0;  // C(n-1, s), exact in fp64 for n <= 40
+  for (int j = 0; j < s; ++j) C = C * (double)(n - 1 - j) / (double)(j + 1);
+  return 1.0 / ((double)n * C);
+}
+
+inline Weights make_weights(int n) {
+  Weights W;
+  for (int s = 0; s < MAX_N + 2; ++s) {
+    W.cw[s] = (s <= n) ? (weight_w(n, s - 1) + weight_w(n, s)) : 0.0;
+    W.bw[s] = (s <= n) ? weight_w(n, s) : 0.0;
+  }
+  return W;
+}
+
+__device__ __forceinline__ void load_weights(const Weights& W, double* cw, double* bw) {
   const int s = threadIdx.x;
   if (s < 64) {
-    double w_s = 0.0, w_prev = 0.0;
-    if (s < n) {
-      double C = 1.0;  // C(n-1, s), exact in fp64 for n <= 40
-      for (int j = 0; j < s; ++j) C = C * (double)(n - 1 - j) / (double)(j + 1);
-      w_s = 1.0 / ((double)n * C);
-    }
-    if (s >= 1 && s - 1 < n) {
-      double C = 1.0;
-      for (int j = 0; j < s - 1; ++j) C = C * (double)(n - 1 - j) / (double)(j + 1);
-      w_prev = 1.0 / ((double)n * C);
-    }
-    cw[s] = (s <= n) ? (w_prev + w_s) : 0.0;
-    bw[s] = (s <= n) ? w_s : 0.0;
+    cw[s] = s < MAX_N + 2 ? W.cw[s] : 0.0;
+    bw[s] = s < MAX_N + 2 ? W.bw[s] : 0.0;
   }
 }
 
+// Pass groups (mask bits 13..15) are split over `gsplit` blocks when a range has few 65536-mask spans, so
+// small tables (n < 24) still launch >= 256 blocks (one per CU); every block's partials are membership sums
+// over its own masks, so the reduction is unchanged.  gsplit = 1 from 256 spans up (a finer split measured
+// slower at n = 24-26: the per-block reductions outweigh the extra parallelism).
+inline int gsplit_for(uint64_t nspans) {
+  int g = 1;
+  while (g < 8 && nspans * (uint64_t)g < 256) g *= 2;
+  return g;
+}
+
 // ------------------------------------------------------------------------------------------------
-// Main pass: one block = 65536 consecutive masks starting at a multiple of 65536.
+// Main pass: one block = 65536 / gsplit masks of a 65536-mask span starting at a multiple of 65536.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(TPB) void shapley_block_kernel(const double* __restrict__ v, uint64_t mask_begin,
-                                                            int n, double* __restrict__ blockpart) {
+                                                            int n, int gsplit, const Weights W,
+                                                            double* __restrict__ blockpart) {
   __shared__ double cw_s[64];
   __shared__ double bw_s[64];
   __shared__ double red_s[4][NQ];
-  build_weights(n, cw_s, bw_s);
+  load_weights(W, cw_s, bw_s);
   __syncthreads();
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const uint64_t base = mask_begin + (uint64_t)blockIdx.x * SPAN;
+  const uint64_t span = blockIdx.x / (unsigned)gsplit;
+  const int gn = 8 / gsplit, g0 = (int)(blockIdx.x % (unsigned)gsplit) * gn;
+  const uint64_t base = mask_begin + span * SPAN;
   // thread-constant mask bits: lane -> bits 1..6, wave -> bits 8..9
   const int s_thread = __popcll(base) + __popc(lane) + __popc(wave);
 
@@ -107,10 +133,10 @@ __global__ __launch_bounds__(TPB) void shapley_block_kernel(const double* __rest
   double a_b0 = 0, a_b0_c = 0, a_b7 = 0, a_b7_c = 0;
   double a_p[6] = {0, 0, 0, 0, 0, 0}, a_p_c[6] = {0, 0, 0, 0, 0, 0};
 
-  const dvec2* vb = reinterpret_cast<const dvec2*>(v + (uint64_t)blockIdx.x * SPAN) + wave * 128 + lane;
+  const dvec2* vb = reinterpret_cast<const dvec2*>(v + span * SPAN) + wave * 128 + lane;
 
   // pass p = 8 g + r: r (mask bits 10..12) unrolled at compile time, g (mask bits 13..15) a uniform loop.
-  for (int g = 0; g < 8; ++g) {
+  for (int g = g0; g < g0 + gn; ++g) {
     const int sg = s_thread + __popc(g);
     double cw[6], bw[6];  // weights for popcount sg + k, k = popc(r) + h + e in [0, 5]
 #pragma unroll
@@ -185,8 +211,8 @@ __global__ __launch_bounds__(TPB) void shapley_block_kernel(const double* __rest
 
 // Reduce per-block partials into partial_out[2*(n+1)] (double-double).  One block per quantity.
 __global__ __launch_bounds__(TPB) void shapley_reduce_blocks_kernel(const double* __restrict__ blockpart,
-                                                                    uint64_t nblocks, uint64_t mask_begin, int n,
-                                                                    double* __restrict__ partial_out) {
+                                                                    uint64_t nblocks, int gsplit, uint64_t mask_begin,
+                                                                    int n, double* __restrict__ partial_out) {
   __shared__ double hs[TPB], ls[TPB];
   const int qi = blockIdx.x;  // 0..n-1 players, n = B
   double s = 0.0, c = 0.0;
@@ -197,7 +223,7 @@ __global__ __launch_bounds__(TPB) void shapley_reduce_blocks_kernel(const double
     } else if (qi < LOG_SPAN) {
       x = blockpart[b * NQ + qi];
     } else {
-      const uint64_t base = mask_begin + b * SPAN;
+      const uint64_t base = mask_begin + (b / (uint64_t)gsplit) * SPAN;
       x = ((base >> qi) & 1ull) ? blockpart[b * NQ + 16] : 0.0;
     }
     two_sum_acc(s, c, x);
@@ -222,11 +248,12 @@ __global__ __launch_bounds__(TPB) void shapley_reduce_blocks_kernel(const double
 
 // Small tables (n < 16, or any range): one block, generic per-element membership loop.
 __global__ __launch_bounds__(TPB) void shapley_small_kernel(const double* __restrict__ v, uint64_t mask_begin,
-                                                            uint64_t count, int n, double* __restrict__ partial_out) {
+                                                            uint64_t count, int n, const Weights W,
+                                                            double* __restrict__ partial_out) {
   __shared__ double cw_s[64];
   __shared__ double bw_s[64];
   __shared__ double hs[TPB], ls[TPB];
-  build_weights(n, cw_s, bw_s);
+  load_weights(W, cw_s, bw_s);
   __syncthreads();
   double as[16], ac[16];
 #pragma unroll
@@ -286,7 +313,8 @@ int mplc_abi_version(void) { return MPLC_ABI_VERSION; }
 
 size_t mplc_shapley_workspace_bytes(int n, uint64_t count) {
   if (n < 16) return 0;
-  return (size_t)((count + SPAN - 1) / SPAN) * NQ * sizeof(double);
+  const uint64_t nspans = (count + SPAN - 1) / SPAN;
+  return (size_t)(nspans * gsplit_for(nspans)) * NQ * sizeof(double);
 }
 
 int mplc_shapley_partial(const double* v, uint64_t mask_begin, uint64_t count, int n, double* partial_out,
@@ -296,18 +324,20 @@ int mplc_shapley_partial(const double* v, uint64_t mask_begin, uint64_t count, i
   if (n < 64 && (mask_begin >= (1ull << n) || count > (1ull << n) - mask_begin)) return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (n < 16) {
-    shapley_small_kernel<<<1, TPB, 0, s>>>(v, mask_begin, count, n, partial_out);
+    shapley_small_kernel<<<1, TPB, 0, s>>>(v, mask_begin, count, n, make_weights(n), partial_out);
     return hip_status();
   }
   if ((mask_begin % SPAN) != 0 || (count % SPAN) != 0) return MPLC_E_ARG;
-  const uint64_t nblocks = count / SPAN;
+  const uint64_t nspans = count / SPAN;
+  const int gsplit = gsplit_for(nspans);
+  const uint64_t nblocks = nspans * gsplit;
   if (workspace == nullptr || workspace_bytes < mplc_shapley_workspace_bytes(n, count)) return MPLC_E_WORKSPACE;
   if (nblocks > 0x7fffffffull) return MPLC_E_ARG;
   double* bp = (double*)workspace;
-  shapley_block_kernel<<<(unsigned)nblocks, TPB, 0, s>>>(v, mask_begin, n, bp);
+  shapley_block_kernel<<<(unsigned)nblocks, TPB, 0, s>>>(v, mask_begin, n, gsplit, make_weights(n), bp);
   int st = hip_status();
   if (st) return st;
-  shapley_reduce_blocks_kernel<<<n + 1, TPB, 0, s>>>(bp, nblocks, mask_begin, n, partial_out);
+  shapley_reduce_blocks_kernel<<<n + 1, TPB, 0, s>>>(bp, nblocks, gsplit, mask_begin, n, partial_out);
   return hip_status();
 }
 

@@ -49,6 +49,7 @@ def test_argument_errors_without_gpu():
     assert h.mplc_shapley_partial(None, 0, 0, 5, None, None, 0, None) == -1
     assert h.mplc_shapley_finalize(None, 0, None, None) == -1
     assert h.mplc_shapley_workspace_bytes(10, 1024) == 0
-    assert h.mplc_shapley_workspace_bytes(20, 1 << 20) == 16 * 18 * 8
+    assert h.mplc_shapley_workspace_bytes(20, 1 << 20) == 16 * 8 * 18 * 8  # 16 spans x 8 pass-group blocks
+    assert h.mplc_shapley_workspace_bytes(28, 1 << 28) == 4096 * 18 * 8  # >= 256 spans: one block each
     with pytest.raises(RuntimeError):
         _native.check(-2, "x")
