@@ -1,11 +1,12 @@
 # A/B kernel-trace of one probe command with two prebuilt libraries: bash scripts/gpu_ab.sh <probe args...>
-# (gpurun_ab/old.so and gpurun_ab/new.so, built on the CPU side; the in-tree library is restored after).
+# (gpurun_ab/old.so and gpurun_ab/new.so, or the names in $AB_VARIANTS, built on the CPU side; the in-tree
+# library is restored after).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 L=distributed-learning-contributivity_amd/mplc/lib/libmplc_hip.so
 cp $L gpurun_ab/keep.so
-for v in old new; do
+for v in ${AB_VARIANTS:-old new}; do
   cp gpurun_ab/$v.so $L
   O=gpurun_out/ab_$v
   rm -rf $O; mkdir -p $O
