@@ -445,10 +445,8 @@ def main():
         if not args.no_shapley_agg:
             agg = bench_shapley(args.n, 10, 2, rank, world)
             agg["roofline"]["traffic"] = pmc_traffic("shapley_block_kernel", wl)
-            # SURVEY 8(d) also asks for N = 20 and 24 (kernel-time GB/s against the same 8 TB/s)
-            agg["smaller_n"] = [{"n": k, "value": r["value"], "ms_per_step": r["ms_per_step"],
-                                 "kernel_gbs": r["roofline"]["achieved"], "frac": r["roofline"]["frac"]}
-                                for k in (20, 24) for r in [bench_shapley(k, 10, 2, rank, world)]]
+            # N = 20..26 are measured with `--leg shapley --n N` (scripts/gpu_bench.sh), not here:
+            # the kernel-trace average of shapley_block_kernel must stay the N=28 launch
             out["shapley_agg"] = agg
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)

@@ -10,4 +10,8 @@ timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python bench.py --no-cpu-baseline > $O/trace.json 2> $O/trace.err && \
 timeout -k 10 400 rocprofv3 --kernel-include-regex "$K" --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python bench.py --no-cpu-baseline > $O/fetch.json 2> $O/fetch.err && \
 timeout -k 10 400 rocprofv3 --kernel-include-regex "$K" --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python bench.py --no-cpu-baseline > $O/write.json 2> $O/write.err
-echo EXIT $?
+rc=$?
+[ $rc -eq 0 ] && for n in 20 22 24 26; do
+  timeout -k 10 120 python bench.py --leg shapley --n $n --no-cpu-baseline > $O/shapley_n$n.json 2>> $O/shapley.err || { rc=$?; break; }
+done
+echo EXIT $rc

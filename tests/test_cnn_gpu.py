@@ -193,6 +193,16 @@ def test_coalition_accuracies_vs_oracle(scenario, engine, odata):
     assert np.max(diff) <= 0.03, (dev, ref)
     assert np.all(dev > 0.5)  # models learn (10 classes: chance = 0.1)
 
+    # north-star gate: the partner ranking by exact Shapley value is identical (3 players, bitmask table)
+    def sv(vals):
+        V = np.zeros(8)
+        for c, v in zip(all7, vals):
+            V[sum(1 << p for p in c)] = v
+        w = {0: 1 / 3, 1: 1 / 6, 2: 1 / 3}  # |S|!(n-|S|-1)!/n! for n = 3
+        return np.array([sum(w[bin(m).count("1")] * (V[m | 1 << i] - V[m]) for m in range(8) if not m >> i & 1)
+                         for i in range(3)])
+    assert np.array_equal(np.argsort(sv(dev)), np.argsort(sv(ref))), (sv(dev), sv(ref))
+
 
 def test_partner_ranking_reference_contrib_test():
     """Port of tests/end_to_end_tests.py:54-73: partner with 10% of the data scores below the 90% partner for
