@@ -2,6 +2,7 @@
 python scripts/probe_train.py [n_coalitions] [epochs] [size] [mnist|cifar]
   mnist: config #3 shape (10 partners, MNIST-shaped synthetic, M=20)
   cifar: config #4 shape (20 partners, CIFAR10-shaped synthetic, M=20)"""
+import hashlib
 import os
 import sys
 import time
@@ -47,7 +48,8 @@ def main():
     reps = n * size
     print(f"warm {t1 - t0:.2f}s; {n} coalitions x {size} partners, E={E}: {t2 - t1:.2f}s "
           f"-> {n / (t2 - t1):.2f} evals/s, {reps / (t2 - t1):.1f} replica-epochs/s; mean acc {v.mean():.3f}; "
-          f"bs {sorted(set(eng.batch_sizes))}, n_p {sorted(set(eng.partner_sizes))[:3]}", flush=True)
+          f"bs {sorted(set(eng.batch_sizes))}, n_p {sorted(set(eng.partner_sizes))[:3]}; "
+          f"v sha1 {hashlib.sha1(np.ascontiguousarray(v, dtype=np.float64).tobytes()).hexdigest()[:12]}", flush=True)
 
 
 if __name__ == "__main__":
