@@ -1,6 +1,6 @@
 """Benchmark driver (contract: one JSON line on rank 0).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--leg train|shapley]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--leg train|shapley|cifar] [--budget-s B]
 
 leg "train" (default; BASELINE.json metric "coalition v(S) evals/sec (MNIST FedAvg)"): BASELINE config #3
   - MNIST CNN, 10 partners, random split ([0.1]*10), FedAvg, exact "Shapley values" over all 1023
@@ -18,12 +18,23 @@ leg "cifar" (BASELINE config #4): CIFAR10 CNN, 20 partners, FedAvg, "TMCS" (defa
   synthetic data with class templates (signal 0.4: accuracy grows with the data a coalition holds, so the
   truncation behaves as on real data; CIFAR10 itself cannot be fetched).  One step = one full
   compute_contributivity(method) with numpy seeded 0; value = distinct coalitions evaluated / second.
+
+Wall-clock budget.  One training step is a whole contributivity computation (about 40 s for config #3 on one
+MI355X), so the driver's `--steps 20 --warmup 5` would not fit its 600 s limit.  The run is held to
+--budget-s seconds from process start (default 480, covering interpreter start, warm-up, the timed steps,
+the N=28 aggregation leg and the CPU baseline): warm-up is capped at one step (it only pays the one-time
+allocation of the lockstep batch), and the timed region runs the largest K' <= K whole steps that the
+measured warm-up step says will fit.  The line reports K' as "steps" (and the requested K as
+"steps_requested"); every timed step is complete, nothing inside a step is skipped.  A heartbeat goes to
+stderr after every step.
 """
 import argparse
 import json
 import os
 import sys
 import time
+
+T_PROC0 = time.perf_counter()  # before `import torch` (its first import on a fresh box can take minutes)
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "distributed-learning-contributivity_amd")
@@ -36,6 +47,26 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (v_mfma_f32_32x32x2_f32
 CONV_BWD_DATA_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2  # dA1 = dZ2 (*) W2 over all conv1 positions
 MNIST_FWD_FLOP = 23984896       # per sample, SURVEY A21
 MNIST_TRAIN_FLOP = 71565312     # per sample (fwd + wgrad + dgrad, no conv1 dgrad)
+TRAFFIC_SOURCE = ("profiles/pmc_traffic.json: FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes of "
+                  "this same command (scripts/pmc_traffic.py), not measured in this run")
+
+
+def log(msg):
+    print(f"[bench {time.perf_counter() - T_PROC0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def host_threads():
+    """Host CPU threads this process may use.  On the GPU box OMP_NUM_THREADS carries the job's CPU share
+    (16 per GPU) while os.cpu_count() reports every core of the shared host, so the smaller one is used."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def pmc_traffic(kernel, workload):
@@ -92,6 +123,43 @@ def sum_over_ranks(x, world):
     return float(t.item())
 
 
+def run_budgeted(warm_step, timed_step, args, world, reserve_s, what):
+    """Warm-up (at most one step of `warm_step`) + timed steps of `timed_step` under the wall-clock budget.
+    Returns (steps run, warm-up steps run, wall seconds of the timed region (max over ranks), the last step's
+    result).  Every rank takes the same decisions: they are made from max-over-ranks times."""
+    warm = min(args.warmup, 1)
+    t_step = 0.0
+    for _ in range(warm):
+        t = time.perf_counter()
+        warm_step()
+        barrier(world)
+        t_step = max_over_ranks(time.perf_counter() - t, world)
+        log(f"{what}: warm-up step {t_step:.1f}s")
+    elapsed = max_over_ranks(time.perf_counter() - T_PROC0, world)
+    left = args.budget_s - elapsed - reserve_s
+    steps = args.steps
+    if t_step > 0:
+        steps = max(1, min(args.steps, int(left // (t_step * 1.03))))
+    log(f"{what}: timing {steps} of {args.steps} requested steps ({left:.0f}s left for them)")
+    barrier(world)
+    t0 = time.perf_counter()
+    res = None
+    done = 0
+    for i in range(steps):
+        ts = time.perf_counter()
+        res = timed_step()
+        done += 1
+        log(f"{what}: step {i + 1}/{steps} {time.perf_counter() - ts:.1f}s")
+        if t_step == 0 and done < steps:
+            # no warm-up estimate: stop early rather than overrun (decided on rank-0's clock, broadcast by max)
+            over = (time.perf_counter() - T_PROC0) + (time.perf_counter() - ts) + reserve_s > args.budget_s
+            if max_over_ranks(1.0 if over else 0.0, world) > 0:
+                break
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    return done, warm, wall, res
+
+
 # --------------------------------------------------------------------------------------------------
 # exact-Shapley aggregation (config #5)
 # --------------------------------------------------------------------------------------------------
@@ -143,6 +211,7 @@ def bench_shapley(n, steps, warmup, rank, world):
     ms_per_step = wall * 1000 / steps
     shard_bytes = (end - begin) * 8
     achieved = shard_bytes / (kern_ms / 1000) / 1e9
+    del V
     return {
         "metric": "exact-Shapley aggregation GB/s at N=%d" % n, "value": round((1 << n) * 8 / (ms_per_step / 1000) / 1e9, 2),
         "unit": "GB/s", "ms_per_step": round(ms_per_step, 4), "n": n, "table_bytes": (1 << n) * 8,
@@ -155,7 +224,7 @@ def bench_shapley(n, steps, warmup, rank, world):
 
 def cpu_baseline_shapley(n_sample=24):
     from oracle import shapley as osh
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     V = osh.synthetic_table(n_sample)
     osh.shapley_bitmask_f64_omp(n_sample, V, threads)
     reps, t0 = 0, time.perf_counter()
@@ -183,46 +252,108 @@ def build_scenario(partners, epochs, M, G):
     return sc.provision()
 
 
-def cpu_baseline_train(sc, epochs, M, budget_s=25.0):
-    """Oracle (torch-CPU fp32, sequential one coalition at a time like the reference) on a bounded stratified
-    sample: one coalition of each size 1, 2, 3 (size 1 = singleton fit); per-partner cost is linear in |S|
-    for FedAvg, so the full 2^n - 1 sweep is extrapolated as sum_k C(n,k) t(k) with t(k) from a line
-    through the measured FedAvg sizes (t(1) measured directly)."""
+def _time_unit(fn, min_s=1.0, max_reps=50):
+    fn()  # first call pays allocator / thread-pool start
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        if time.perf_counter() - t0 >= min_s or reps >= max_reps:
+            break
+    return (time.perf_counter() - t0) / reps
+
+
+def cpu_baseline_train(sc, epochs, M):
+    """CPU baseline for config #3: the oracle (torch-CPU fp32 restatement of the
+    reference's Keras path, sequential, one coalition at a time, a fresh Keras Adam per partner fit) on the
+    host's CPU share.  A whole 1023-coalition sweep takes hours on CPU, and one coalition of every size
+    class still takes many minutes, so the bounded sample (~30 s) times the UNITS a sequential sweep is made
+    of and sums them over every coalition in closed form:
+      t_fit    one partner's FedAvg round: fresh model + Adam, ~9 Keras steps at bs_p on its minibatch
+               (mplc/multi_partner_learning.py:301-334), averaged over the partners
+      t_agg(k) the data-volume np.average of k models (mplc/mpl_utils.py:90-102), linear in k
+      t_val    one evaluate on the 6000-sample val set; t_test one evaluate on the 10000-sample test set
+      t_epoch  one singleton epoch: full partner data at bs_p, persistent Adam (:238-269)
+    lean:      |S|>=2: E*M*(|S|*t_fit + t_agg(|S|)) + t_test;   |S|=1: E*t_epoch + t_test
+    faithful:  adds the reference's per-round global-val evaluate and every partner fit's Keras
+               validation_data evaluate, E*M*(|S|+1)*t_val (singletons: E*t_val)
+    and checks the model against one real coalition {0,1} trained end to end (E=1, lean)."""
     import numpy as np
     import torch
     from math import comb
     from oracle import cnn as ocnn
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
+    t_all = time.perf_counter()
     ds = sc.dataset
     data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow = [p.train_idx for p in sc.partners_list]
-    bs = [p.batch_size for p in sc.partners_list]
+    bs = [int(p.batch_size) for p in sc.partners_list]
     n = len(prow)
-    times = {}
-    t_all = time.perf_counter()
-    for k in (1, 2, 3):
-        t0 = time.perf_counter()
-        ocnn.coalition_value(data, prow, bs, tuple(range(k)), epochs=epochs, M=M)
-        times[k] = time.perf_counter() - t0
-        if time.perf_counter() - t_all > budget_s and k >= 2:
-            break
-    ks = sorted(k for k in times if k >= 2)
-    if len(ks) >= 2:
-        slope = (times[ks[-1]] - times[ks[0]]) / (ks[-1] - ks[0])
-        icpt = times[ks[0]] - slope * ks[0]
-    else:
-        slope, icpt = times[2] / 2.0, 0.0
-    total = sum(comb(n, k) * (times[1] if k == 1 else icpt + slope * k) for k in range(1, n + 1))
-    return {"value": round((2 ** n - 1) / total, 5), "unit": "coalition evals/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle torch-CPU fp32 sequential FedAvg/singleton fits of coalitions of size 1,2,3 "
-                       f"(E={epochs}, M={M}): {', '.join(f'|S|={k}: {v:.1f}s' for k, v in sorted(times.items()))}; "
-                       f"full {2 ** n - 1}-coalition sweep extrapolated linearly in |S|: {total:.0f}s")}
+    sizes = np.array([len(r) for r in prow], dtype=np.float64)
+    glob = ocnn.unpack(ocnn.init_params(ocnn.init_key(0, (1 << n) - 1)))
+    fits = [0]
+
+    def fit_round():
+        p = fits[0] % n
+        fits[0] += 1
+        key = ocnn.shuffle_key(0, (1 << n) - 1, p)
+        params = {k: v.clone() for k, v in glob.items()}
+        opt = ocnn.KerasAdam(params)
+        for rows in ocnn.fedavg_round_rows(key, prow[p], bs[p], M, 0, fits[0] % M):
+            g, _ = ocnn.gradients(params, data.x_train[rows], data.y_train[rows])
+            opt.step(params, g)
+        return params
+
+    t_fit = _time_unit(fit_round, min_s=3.0)
+    models = [fit_round() for _ in range(n)]
+    t_agg2 = _time_unit(lambda: ocnn.average_models(glob, models[:2], sizes[:2] / sizes[:2].sum()), 0.5)
+    t_aggn = _time_unit(lambda: ocnn.average_models(glob, models, sizes / sizes.sum()), 0.5)
+    t_val = _time_unit(lambda: ocnn.evaluate(glob, data.x_val, data.y_val), 1.0, 5)
+    t_test = _time_unit(lambda: ocnn.evaluate(glob, data.x_test, data.y_test), 1.0, 5)
+
+    def single_epoch():
+        params = {k: v.clone() for k, v in glob.items()}
+        opt = ocnn.KerasAdam(params)
+        for rows in ocnn.single_epoch_rows(ocnn.shuffle_key(0, 1, 0), prow[0], bs[0], 0):
+            g, _ = ocnn.gradients(params, data.x_train[rows], data.y_train[rows])
+            opt.step(params, g)
+    t0 = time.perf_counter()
+    single_epoch()
+    t_epoch = time.perf_counter() - t0
+
+    def t_agg(k):
+        return t_agg2 + (t_aggn - t_agg2) * (k - 2) / max(1, n - 2)
+
+    lean = faithful = 0.0
+    for k in range(1, n + 1):
+        if k == 1:
+            c_lean = epochs * t_epoch + t_test
+            c_faith = c_lean + epochs * t_val
+        else:
+            c_lean = epochs * M * (k * t_fit + t_agg(k)) + t_test
+            c_faith = c_lean + epochs * M * (k + 1) * t_val
+        lean += comb(n, k) * c_lean
+        faithful += comb(n, k) * c_faith
+    # model check: one real coalition, E=1, lean schedule, end to end
+    t0 = time.perf_counter()
+    ocnn.coalition_value(data, prow, bs, (0, 1), epochs=1, M=M)
+    t_pair = time.perf_counter() - t0
+    pair_model = M * (2 * t_fit + t_agg(2)) + t_test
+    n_coal = 2 ** n - 1
+    return {"value": round(n_coal / lean, 5), "unit": "coalition evals/s", "cores": threads, "kind": "port",
+            "faithful_value": round(n_coal / faithful, 6),
+            "method": "unit-timed closed-form sum over all coalitions (bench.py cpu_baseline_train docstring)",
+            "sample": (f"oracle torch-CPU fp32, {threads} threads, {time.perf_counter() - t_all:.0f}s of CPU work: "
+                       f"t_fit {t_fit * 1e3:.0f} ms/partner-round, t_agg {t_agg2 * 1e3:.0f}-{t_aggn * 1e3:.0f} ms "
+                       f"(2-{n} models), t_val {t_val:.2f}s, t_test {t_test:.2f}s, singleton epoch {t_epoch:.2f}s; "
+                       f"sweep (E={epochs}, M={M}, {n_coal} coalitions) lean {lean:.0f}s, reference-faithful "
+                       f"(+ per-round global-val and per-fit validation_data evals) {faithful:.0f}s; "
+                       f"check: coalition (0,1) at E=1 measured {t_pair:.1f}s vs modelled {pair_model:.1f}s")}
 
 
 def bench_train(args, rank, world):
     import numpy as np
-    import torch
     from mplc.contributivity import Contributivity
     from mplc.profiling import KernelTimer
     sc = build_scenario(args.partners, args.epochs, args.minibatches, args.gupp)
@@ -232,6 +363,7 @@ def bench_train(args, rank, world):
     eng.warmup()  # untimed: code-object load (no training launch, so rocprof averages = timed launches)
     n = args.partners
     n_coal = 2 ** n - 1
+    log(f"train leg ready: {n} partners, {n_coal} coalitions")
 
     def one_step():
         sc.coalition_values = {}  # retrain every coalition each step
@@ -239,22 +371,22 @@ def bench_train(args, rank, world):
         c.compute_contributivity("Shapley values")
         return c
 
-    for _ in range(args.warmup):
-        one_step()
-    barrier(world)
     timer = KernelTimer(args.profile_kernel)
-    eng.profiler = timer
-    reps0 = eng.stats["replicas"]
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        c = one_step()
-    barrier(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
+    reps0 = [0]
+
+    def timed_step():
+        if eng.profiler is None:  # the timed region starts: attach the in-stream kernel timer
+            eng.profiler = timer
+            reps0[0] = eng.stats["replicas"]
+        return one_step()
+
+    # reserve: the N=28 aggregation leg (~10 s with its table) and, at N=1, the bounded CPU baseline (~40 s)
+    reserve = (0 if args.no_shapley_agg else 15) + (45 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
+    steps, warm, wall, c = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     kern_ms = timer.total_ms()
     launches = timer.launches()
-    # algorithmic work of the profiled kernel on THIS rank: every replica sees its n_p rows once per epoch
-    local_reps = eng.stats["replicas"] - reps0
+    local_reps = eng.stats["replicas"] - reps0[0]
     sizes = eng.partner_sizes
     # exact per-rank sample count: sum over this rank's replicas of E * n_p (shard is LPT over coalitions)
     from mplc.parallel import lpt_shard, coalition_cost
@@ -262,15 +394,15 @@ def bench_train(args, rank, world):
     coals = [cc for r in range(1, n + 1) for cc in combinations(range(n), r)]
     shards = lpt_shard([coalition_cost(cc, sizes) for cc in coals], world)
     mine = [coals[i] for i in shards[rank]]
-    samples = args.steps * args.epochs * sum(sizes[p] for cc in mine for p in cc)
+    samples = steps * args.epochs * sum(sizes[p] for cc in mine for p in cc)
     flops = samples * CONV_BWD_DATA_FLOP_PER_SAMPLE
     achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
-    ms_per_step = wall * 1000 / args.steps
+    ms_per_step = wall * 1000 / steps
     total_train_samples = sum_over_ranks(samples, world)
     out = {
         "metric": "coalition v(S) evals/sec (MNIST FedAvg)",
-        "value": round(n_coal * args.steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 1), "higher_is_better": True,
+        "value": round(n_coal * steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
+        "steps": steps, "warmup": warm, "ms_per_step": round(ms_per_step, 1), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (MNIST-shaped: x~U[0,1) fp32 [60000,28,28,1], random one-hot labels)",
         "config": {"workload": f"BASELINE config #3: MNIST CNN, {n} partners random split, FedAvg, exact Shapley "
@@ -278,9 +410,12 @@ def bench_train(args, rank, world):
                                f"G={args.gupp}), coalitions LPT-sharded x{world}",
                    "partners": n, "coalitions": n_coal, "epochs": args.epochs, "minibatch_count": args.minibatches,
                    "gradient_updates_per_pass": args.gupp, "batch_size": [int(p.batch_size) for p in sc.partners_list],
-                   "replicas_trained_per_step": int(sum_over_ranks(local_reps, world) / max(1, args.steps)),
-                   "train_samples_per_step": int(total_train_samples / args.steps),
+                   "replicas_trained_per_step": int(sum_over_ranks(local_reps, world) / max(1, steps)),
+                   "train_samples_per_step": int(total_train_samples / steps),
                    "parallelism": f"coalition-shard x{world}"},
+        "budget": {"budget_s": args.budget_s, "steps_requested": args.steps, "warmup_requested": args.warmup,
+                   "timed_wall_s": round(wall, 2), "note": "one step = one whole 1023-coalition sweep; K clamped to "
+                                                          "the whole steps that fit the wall-clock budget"},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                      "kernel": f"{args.profile_kernel}_kernel", "launches": launches,
@@ -295,7 +430,7 @@ def bench_train(args, rank, world):
     }
     # whole-job algorithmic rate: training 2*E*sum n_p samples x 71.57 MFLOP + test evaluation
     # 1023 x 10000 x 23.98 MFLOP (MNIST CNN forward / train FLOPs per sample)
-    job_flop = total_train_samples / args.steps * MNIST_TRAIN_FLOP + n_coal * len(sc.dataset.x_test) * MNIST_FWD_FLOP
+    job_flop = total_train_samples / steps * MNIST_TRAIN_FLOP + n_coal * len(sc.dataset.x_test) * MNIST_FWD_FLOP
     out["algorithmic"] = {"flop_per_step": int(job_flop), "tflops": round(job_flop / (ms_per_step / 1000) / 1e12, 2),
                           "frac_of_fp32_mfma_peak": round(job_flop / (ms_per_step / 1000) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
     return out, sc
@@ -314,12 +449,12 @@ def build_cifar_scenario(epochs, signal):
     return sc.provision()
 
 
-def cpu_baseline_cifar(sc, coalitions, epochs, M, budget_s=25.0):
+def cpu_baseline_cifar(sc, coalitions, epochs, M):
     """Oracle (torch-CPU fp32, sequential like the reference) on a bounded sample: one singleton and one
     pair; FedAvg cost is linear in |S|, so the evaluated coalition list is extrapolated from t(1), t(2)."""
     import torch
     from oracle import cifar_cnn as occ
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     ds = sc.dataset
     data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
@@ -348,13 +483,13 @@ def bench_cifar(args, rank, world):
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
     eng.warmup()
-    t_start = time.perf_counter()
 
     def progress(s, total, R):  # the run is long: keep a heartbeat on stderr
         if s == 0:
-            print(f"[bench cifar {time.perf_counter() - t_start:7.1f}s] batch of {R} replicas, {total} steps, "
-                  f"{eng.stats['coalitions']} coalitions so far", file=sys.stderr, flush=True)
+            log(f"cifar: batch of {R} replicas, {total} steps, {eng.stats['coalitions']} coalitions so far")
     eng.progress = progress
+    timer = KernelTimer(args.cifar_profile_kernel)
+    s0 = [0]
 
     def one_step():
         sc.coalition_values = {}
@@ -363,38 +498,38 @@ def bench_cifar(args, rank, world):
         c.compute_contributivity(args.method)
         return c
 
-    for _ in range(args.warmup):
-        one_step()
-    barrier(world)
-    timer = KernelTimer(args.cifar_profile_kernel)
-    eng.profiler = timer
-    s0 = eng.stats["samples"]
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        c = one_step()
-    barrier(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
+    def timed_step():
+        if eng.profiler is None:
+            eng.profiler = timer
+            s0[0] = eng.stats["samples"]
+        return one_step()
+
+    reserve = (60 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
+    steps, warm, wall, c = run_budgeted(one_step, timed_step, args, world, reserve, "cifar")
     eng.profiler = None
     kern_ms = timer.total_ms()
     launches = timer.launches()
-    samples = eng.stats["samples"] - s0
+    samples = eng.stats["samples"] - s0[0]
     flops = samples * FLOP_PER_SAMPLE[args.cifar_profile_kernel]
     achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
     evals = c.first_charac_fct_calls_count
     coals = [k for k in c.charac_fct_values if len(k)]
     out = {
         "metric": f"coalition v(S) evals/sec (CIFAR10 FedAvg, {args.method})",
-        "value": round(evals * args.steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1000 / args.steps, 1),
+        "value": round(evals * steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
+        "steps": steps, "warmup": warm, "ms_per_step": round(wall * 1000 / steps, 1),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (CIFAR10-shaped: x = 0.4 class template + 0.6 U[0,1) fp32 [50000,32,32,3], one-hot labels)",
         "config": {"workload": f"BASELINE config #4: CIFAR10 CNN, 20 partners, FedAvg, {args.method} (reference defaults, "
                                f"numpy seed 0), E={args.cifar_epochs} fixed, M=20, G=8, coalitions LPT-sharded x{world}",
                    "partners": 20, "method": args.method, "coalitions_evaluated": evals,
                    "coalition_sizes": {str(k): sum(1 for c_ in coals if len(c_) == k) for k in range(1, 21)},
-                   "train_samples_per_step_this_rank": int(samples / max(1, args.steps)),
+                   "train_samples_per_step_this_rank": int(samples / max(1, steps)),
                    "shapley_estimate": [round(float(v), 5) for v in c.contributivity_scores],
+                   "replicas_per_launch": eng.stats.get("replicas", 0) / max(1, eng.stats.get("batches", 1)),
                    "parallelism": f"coalition-shard x{world}"},
+        "budget": {"budget_s": args.budget_s, "steps_requested": args.steps, "warmup_requested": args.warmup,
+                   "timed_wall_s": round(wall, 2)},
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                      "kernel": args.cifar_profile_kernel, "launches": launches,
@@ -408,8 +543,10 @@ def bench_cifar(args, rank, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--budget-s", type=float, default=480.0,
+                    help="wall-clock budget from process start for the whole run (driver limit: 600 s)")
     ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar"])
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
@@ -442,15 +579,21 @@ def main():
         out, sc = bench_train(args, rank, world)
         wl = out["config"]["workload"]
         out["roofline"]["traffic"] = pmc_traffic(f"{args.profile_kernel}_kernel", wl)
+        out["roofline"]["traffic_source"] = TRAFFIC_SOURCE
         if not args.no_shapley_agg:
+            # the lockstep training batch's buffers are no longer needed: give the 2 GiB table room
+            sc.engine.release()
             agg = bench_shapley(args.n, 10, 2, rank, world)
             agg["roofline"]["traffic"] = pmc_traffic("shapley_block_kernel", wl)
+            agg["roofline"]["traffic_source"] = TRAFFIC_SOURCE
             # N = 20..26 are measured with `--leg shapley --n N` (scripts/gpu_bench.sh), not here:
             # the kernel-trace average of shapley_block_kernel must stay the N=28 launch
             out["shapley_agg"] = agg
+            log(f"shapley_agg N={args.n}: {agg['value']} GB/s")
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
                                    if (world == 1 and not args.no_cpu_baseline) else None)
+    out["wall_s_total"] = round(time.perf_counter() - T_PROC0, 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

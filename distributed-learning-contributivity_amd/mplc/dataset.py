@@ -9,8 +9,12 @@ The images themselves: MNIST is loaded from a local keras-format ``mnist.npz`` (
 x_test, y_test) found via $MPLC_DATA_DIR, ./data or ~/.keras/datasets - the reference downloads it
 (mplc/dataset.py:415-440), which is impossible offline.  Without a local file, ``Mnist(synthetic=True)``
 builds tensors of MNIST's exact shapes (x ~ U[0,1) float32 [60000,28,28,1], one-hot labels) for
-throughput work; ``synthetic`` records which one was used.
+throughput work; ``synthetic`` records which one was used.  Synthetic data are never substituted silently:
+with ``synthetic=None`` (the default, and what Scenario(dataset_name=...) and the CLI use) a missing file
+raises FileNotFoundError unless MPLC_SYNTHETIC_DATA=1 opts in, which logs a warning (and results.csv
+carries a ``synthetic_data`` column).
 """
+import logging
 import os
 
 import numpy as np
@@ -84,6 +88,19 @@ def _local_mnist():
     return None
 
 
+def _synthetic_allowed(synthetic, what):
+    """True: build synthetic data.  synthetic=True asks for it; synthetic=None (no local file found) only
+    with MPLC_SYNTHETIC_DATA=1; otherwise the missing file is an error, never a silent substitution."""
+    if synthetic:
+        return True
+    if synthetic is None and os.environ.get("MPLC_SYNTHETIC_DATA", "") == "1":
+        logging.getLogger("mplc").warning(f"{what} not found: using SYNTHETIC data of the same shape "
+                                          "(MPLC_SYNTHETIC_DATA=1); the results do not describe the real dataset")
+        return True
+    raise FileNotFoundError(f"{what} not found (set MPLC_DATA_DIR, or pass synthetic=True / set "
+                            "MPLC_SYNTHETIC_DATA=1 for shape-identical synthetic data); no network to download it")
+
+
 def _one_hot(y, k):
     return np.eye(k, dtype="float32")[np.asarray(y, dtype=np.int64).ravel()]
 
@@ -109,12 +126,15 @@ def _synthetic_images(shape, n_train, n_test, seed, signal=0.0):
 class Mnist(Dataset):
     """mplc/dataset.py:397-488 (model: the engine's batched CNN of the same architecture)."""
 
-    def __init__(self, synthetic=None, seed=0, n_train=60000, n_test=10000):
+    def __init__(self, synthetic=None, seed=0, n_train=60000, n_test=10000, signal=0.0):
         self.img_rows = self.img_cols = 28
         loaded = None if synthetic else _local_mnist()
         if loaded is None:
-            if synthetic is False:
-                raise FileNotFoundError("mnist.npz not found (set MPLC_DATA_DIR); no network to download it")
+            _synthetic_allowed(synthetic, "mnist.npz")
+        if loaded is None and signal > 0:  # learnable: class templates + noise (see _synthetic_images)
+            x_train, y_train, x_test, y_test = _synthetic_images((28, 28, 1), n_train, n_test, seed, signal)
+            self.synthetic = True
+        elif loaded is None:
             rng = np.random.default_rng(seed)
             x_train = rng.random((n_train, 28, 28, 1), dtype=np.float32)
             x_test = rng.random((n_test, 28, 28, 1), dtype=np.float32)
@@ -158,8 +178,7 @@ class Cifar10(Dataset):
     def __init__(self, synthetic=None, seed=0, n_train=50000, n_test=10000, signal=0.0):
         loaded = None if synthetic else _local_npz("cifar10.npz")
         if loaded is None:
-            if synthetic is False:
-                raise FileNotFoundError("cifar10.npz not found (set MPLC_DATA_DIR); no network to download it")
+            _synthetic_allowed(synthetic, "cifar10.npz")
             x_train, y_train, x_test, y_test = _synthetic_images((32, 32, 3), n_train, n_test, seed, signal)
             self.synthetic = True
         else:
@@ -218,8 +237,7 @@ class Titanic(Dataset):
                     xdf = xdf.drop(["Name", "Pclass", "Siblings/Spouses Aboard", "Parents/Children Aboard", "Title"],
                                    axis=1)
                     return xdf.to_numpy(dtype="float32"), raw["Survived"].to_numpy(dtype="float32"), False
-        if synthetic is False:
-            raise FileNotFoundError("titanic.csv not found (set MPLC_DATA_DIR); no network to download it")
+        _synthetic_allowed(synthetic, "titanic.csv")
         from sklearn.datasets import make_classification
         X, y = make_classification(n_samples=887, n_features=27, n_informative=8, random_state=0)
         return X.astype("float32"), y.astype("float32"), True

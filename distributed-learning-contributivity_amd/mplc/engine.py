@@ -86,7 +86,10 @@ class CoalitionEngine:
         self.splits_d = torch.tensor(splits, dtype=torch.int32, device=self.device)
         if memory_budget_bytes is None:
             free, _ = torch.cuda.mem_get_info(self.device)
-            memory_budget_bytes = int(free * 0.8) - self.eval_budget_bytes
+            # memory the caching allocator holds but no tensor uses (an earlier engine's lockstep batches) is
+            # as good as free for this engine's batches; mem_get_info does not count it
+            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+            memory_budget_bytes = max(int(free * 0.8) - self.eval_budget_bytes, 1 << 30)
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): HIP events around one kernel per step
@@ -157,6 +160,13 @@ class CoalitionEngine:
         keys = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.model_impl.init_params(buf, keys, _native.stream_handle(self.device))
         torch.cuda.synchronize(self.device)
+
+    def release(self):
+        """Return the cached device memory of finished lockstep batches to the driver (the data stay)."""
+        import gc
+        import torch
+        gc.collect()
+        torch.cuda.empty_cache()
 
     supports_history = True
 

@@ -281,6 +281,8 @@ class Scenario:
             "mpl_nb_epochs_done": self.mpl.history.nb_epochs_done,
             "learning_computation_time_sec": self.mpl.learning_computation_time,
         }
+        if getattr(self.dataset, "synthetic", False):  # not a reference column: only present when true
+            base["synthetic_data"] = True
         rows = []
         if not self.contributivity_list:
             rows.append(dict(base))

@@ -108,3 +108,24 @@ def test_oracle_keyed_perm_is_a_permutation():
     for n in (1, 2, 3, 43, 44, 437, 4374, 30573):
         out = ocnn.keyed_perm(0x1234567 + n, n, np.arange(n))
         assert sorted(out.tolist()) == list(range(n))
+
+
+def test_missing_dataset_is_an_error_not_synthetic(monkeypatch, tmp_path):
+    """a missing mnist.npz / cifar10.npz / titanic.csv raises unless synthetic data are asked for
+    (synthetic=True, or MPLC_SYNTHETIC_DATA=1 which logs a warning and flags results.csv)."""
+    import pytest
+    from mplc import dataset as dm
+    monkeypatch.setenv("MPLC_DATA_DIR", str(tmp_path))
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("HOME", str(tmp_path))
+    monkeypatch.delenv("MPLC_SYNTHETIC_DATA", raising=False)
+    for cls in (dm.Titanic,):
+        with pytest.raises(FileNotFoundError):
+            cls()
+    with pytest.raises(FileNotFoundError):
+        dm.Mnist(n_train=100, n_test=10)
+    with pytest.raises(FileNotFoundError):
+        dm.Cifar10(n_train=100, n_test=10)
+    assert dm.Mnist(synthetic=True, n_train=100, n_test=10).synthetic
+    monkeypatch.setenv("MPLC_SYNTHETIC_DATA", "1")
+    assert dm.Titanic().synthetic
