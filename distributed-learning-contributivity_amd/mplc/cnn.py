@@ -453,7 +453,7 @@ class CnnBatchTrainer:
         fed = [ci for ci in range(C) if not st.coal_is_single[ci]]
         use_es = early_stopping and epochs > PATIENCE
         epochs_done = np.full(C, epochs, dtype=np.int64)
-        val_hist = [[] for _ in range(C)]
+        val_hist = [[] for _ in range(C)]  # per coalition: the val losses the stopping rule compared
         es_best = np.full(C, np.inf)
         es_wait = np.zeros(C, dtype=np.int64)
         spe = {ci: -(-sizes[coalitions[ci][0]] // eng.batch_sizes[coalitions[ci][0]])
@@ -492,6 +492,7 @@ class CnnBatchTrainer:
                 if ends:
                     for ci, l in zip(ends, self._val_loss(st.params, [st.coal_first[c] for c in ends])):
                         e = (s + 1) // spe[ci] - 1
+                        val_hist[ci].append(l)
                         if l < es_best[ci]:
                             es_best[ci], es_wait[ci] = l, 0
                         else:
@@ -504,6 +505,7 @@ class CnnBatchTrainer:
         if rec is not None:
             rec.finish(epochs_done[0])
         glob = st.finalize()
+        self.last_es_trace = val_hist
         correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
         return correct / float(eng.y_test_d.numel()), epochs_done
 

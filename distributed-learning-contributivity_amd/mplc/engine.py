@@ -182,6 +182,7 @@ class CoalitionEngine:
         es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
         scores = np.zeros(len(coalitions))
         epochs_done = np.zeros(len(coalitions), dtype=np.int64)
+        es_trace = [[] for _ in coalitions]
         history = None
         if record_history:
             if len(coalitions) != 1:
@@ -192,6 +193,8 @@ class CoalitionEngine:
             s, e = self.trainer.run(coal, E, es, history=history)
             scores[batch] = s
             epochs_done[batch] = e
+            for i, tr in zip(batch, getattr(self.trainer, "last_es_trace", [[]] * len(batch))):
+                es_trace[i] = list(tr)
             self.stats["batches"] += 1
             self.stats["replicas"] += sum(len(c) for c in coal)
             # samples trained (every replica sees all its partner's rows once per epoch done)
@@ -199,7 +202,9 @@ class CoalitionEngine:
                                              for c, ep in zip(coal, e)))
         self.stats["coalitions"] += len(coalitions)
         if return_details:
-            out = {"scores": scores, "epochs_done": epochs_done}
+            # es_val_loss: the val losses the early-stopping rule compared (start-of-epoch global model for
+            # FedAvg, end-of-epoch model for singletons); empty when early stopping is inactive
+            out = {"scores": scores, "epochs_done": epochs_done, "es_val_loss": es_trace}
             if history is not None:
                 out["history"] = history
             return out

@@ -286,9 +286,10 @@ HISTORY_METRICS = ("val_accuracy", "val_loss", "loss", "accuracy")
 
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
                     aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg",
-                    history=None):
+                    history=None, es_trace=None):
     """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init and order.
-    With a `history` dict, the learning history (mplc/mpl_utils.py:11-27) is recorded into it."""
+    With a `history` dict, the learning history (mplc/mpl_utils.py:11-27) is recorded into it; with an
+    `es_trace` list, the val losses the early-stopping rule compares are appended to it."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
     mask = sum(1 << p for p in coalition)
@@ -315,6 +316,8 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                 opt.step(params, g)
             if early_stopping and epochs > PATIENCE:
                 vl, _ = evaluate(params, data.x_val, data.y_val)
+                if es_trace is not None:
+                    es_trace.append(vl)
                 if vl < best:
                     best, wait = vl, 0
                 else:
@@ -335,6 +338,8 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
         for e in range(epochs):
             if early_stopping and epochs > PATIENCE:
                 val_hist.append(evaluate(glob, data.x_val, data.y_val)[0])
+                if es_trace is not None:
+                    es_trace.append(val_hist[-1])
             for m in range(M):
                 if history is not None:  # round-start collective model (eval_and_log_model_val_perf)
                     vl, va = evaluate(glob, data.x_val, data.y_val)

@@ -227,11 +227,63 @@ def test_scenario_run_end_to_end():
     assert abs(np.sum(sv.contributivity_scores) - sc.mpl.history.score) < 1e-9  # efficiency: sum SV = v(N)
 
 
-def test_early_stopping_path_runs():
-    """E > PATIENCE with early stopping: val evals per epoch, coalitions may stop; epochs_done recorded."""
+def _keras_early_stopping(losses, patience=ocnn.PATIENCE):
+    """Keras 2.3.1 EarlyStopping(monitor='val_loss', patience, min_delta=0) as SinglePartnerLearning uses it
+    (mplc/multi_partner_learning.py:247-260): epochs run."""
+    best, wait = np.inf, 0
+    for e, l in enumerate(losses):
+        if l < best:
+            best, wait = l, 0
+        else:
+            wait += 1
+            if wait >= patience:
+                return e + 1
+    return None
+
+
+def _fedavg_early_stop(losses, patience=ocnn.PATIENCE):
+    """MultiPartnerLearning.early_stop (mplc/multi_partner_learning.py:177-193): stop after epoch e >= patience
+    when val_loss[e, 0] > val_loss[e - patience, 0]: epochs run."""
+    for e in range(patience, len(losses)):
+        if losses[e] > losses[e - patience]:
+            return e + 1
+    return None
+
+
+def test_early_stopping_matches_reference_rule_and_oracle():
+    """Early stopping is on for every Contributivity v(S) (mplc/contributivity.py:101-112).  E=25 on the digits
+    data, where every coalition stops early.
+    - The rule, exactly: the epoch each coalition stopped at is what the reference's rule gives on the val
+      losses the engine compared (FedAvg: start-of-epoch loss vs 10 epochs back; singleton: Keras
+      EarlyStopping with patience 10).
+    - The trajectory: those val losses follow the oracle's over the first epochs (5 %), before fp32
+      summation-order noise takes over (Adam's first steps move every weight by ~lr * sign(g), so weights
+      whose gradient is ~0 take either sign: the oracle itself on 8 vs 16 CPU threads gives 0.3627 vs 0.3669
+      for (0, 1) after one epoch; the engine gave 0.3627).  The stopping epoch itself depends on near-ties of a flat val-loss
+      curve: the oracle run with 8 vs 3 CPU threads stops (0,) at 16 vs 18 and (0, 1) at 19 vs 17.  So the
+      engine's stopping epochs must be within 3 of the oracle's, and v(S) within 3 pt each."""
     from mplc.engine import CoalitionEngine
-    sc = make_scenario(partners=2, amounts=(0.5, 0.5), M=1, G=2, E=12, es=True)
+    E = 25
+    sc = make_scenario(partners=2, amounts=(0.3, 0.7), M=2, G=8, E=E, es=True)
     eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
-    res = eng.evaluate([(0,), (0, 1)], return_details=True)
-    assert np.all(res["epochs_done"] >= 1) and np.all(res["epochs_done"] <= 12)
-    assert np.all(res["scores"] > 0.5)
+    coals = [(0,), (1,), (0, 1)]
+    res = eng.evaluate(coals, return_details=True)
+    ds = sc.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow, bs = rows(sc)
+    for i, c in enumerate(coals):
+        trace = res["es_val_loss"][i]
+        rule = _keras_early_stopping if len(c) == 1 else _fedavg_early_stop
+        stop = rule(trace)
+        assert stop is not None and stop < E, (c, trace)
+        assert res["epochs_done"][i] == stop and len(trace) == stop, (c, res["epochs_done"][i], stop, trace)
+        ref_trace = []
+        ref_acc, ref_ep = ocnn.coalition_value(data, prow, bs, c, seed=eng.seed, epochs=E, M=2, early_stopping=True,
+                                               es_trace=ref_trace)
+        assert ref_ep < E
+        # FedAvg's first entry is the untrained model's val loss: same weights, so equal to fp32 summation order
+        if len(c) > 1:
+            assert abs(trace[0] - ref_trace[0]) <= 1e-5 * ref_trace[0], (c, trace[0], ref_trace[0])
+        assert np.allclose(trace[:3], ref_trace[:3], rtol=5e-2, atol=0), (c, trace[:3], ref_trace[:3])
+        assert abs(int(res["epochs_done"][i]) - ref_ep) <= 3, (c, res["epochs_done"][i], ref_ep)
+        assert abs(res["scores"][i] - ref_acc) <= 0.03, (c, res["scores"][i], ref_acc)

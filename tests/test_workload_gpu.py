@@ -1,0 +1,148 @@
+"""GPU: BASELINE configs #3 and #4 at workload size (not toy sizes).
+
+Config #3 - MNIST CNN, 10 partners, random split, FedAvg, exact "Shapley values" over all 1023 coalitions,
+M=20, G=8 (E=1 here to keep the test near 20 s; the bench runs E=2).  All 1023 coalitions = 5120 replicas
+train as ONE lockstep batch.  Checks:
+  - efficiency: sum of the Shapley values = v(N) (to 1e-12; v(empty) = 0, mplc/contributivity.py:1210-1253);
+  - batch invariance: coalitions re-evaluated alone give bit-identical values to the 5120-replica batch;
+  - |S| in {1, 2} coalitions against the oracle (oracle/cnn.py, sequential like the reference): within 1 pt
+    on average over six coalitions, 3 pt each (10000 test samples: 1 pt = 100 samples).  One epoch leaves the
+    models in the steep part of learning, where fp32 summation order alone moves a single coalition's
+    accuracy by about a point: the oracle itself, run with 8 vs 3 CPU threads, gives 0.9675 vs 0.9793 for
+    (0, 9) and 0.8766 (8 threads here) vs 0.8632 (16 threads on the GPU box) for (2, 7) at signal 0.2;
+  - the memo holds every coalition once (first_charac_fct_calls_count = 1023).
+Config #4 - CIFAR10 CNN, 20 partners ([0.05]*19 + [1 - 0.95], the reference's sum check), FedAvg, TMCS with
+the reference's defaults (sv_accuracy .01, alpha .95, truncation .05, numpy seed 0), E=1, M=20, G=8.  The
+v(S) values the batched engine produced are then fed to the plain host estimator (the reference's
+sequential loop, one coalition at a time, no planning): scores, std, call count and memo must be identical
+(mplc/contributivity.py:195-253 / :92-136).  Two coalitions are compared with oracle/cifar_cnn.py.
+Data: learnable synthetic images of the datasets' exact shapes (class templates + noise, mplc.dataset
+_synthetic_images) - MNIST / CIFAR10 cannot be downloaded here."""
+import types
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mnist10():
+    from mplc.dataset import Mnist
+    from mplc.scenario import Scenario
+    sc = Scenario(10, [0.1] * 10, dataset=Mnist(synthetic=True, signal=0.2), minibatch_count=20,
+                  gradient_updates_per_pass_count=8, epoch_count=1, is_early_stopping=False)
+    return sc.provision()
+
+
+@pytest.fixture(scope="module")
+def config3_sweep(mnist10):
+    from mplc.contributivity import Contributivity
+    c = Contributivity(scenario=mnist10)
+    c.compute_contributivity("Shapley values")
+    return c, mnist10.engine
+
+
+def test_config3_one_lockstep_batch_and_efficiency(mnist10, config3_sweep):
+    c, eng = config3_sweep
+    assert eng.stats["batches"] == 1 and eng.stats["replicas"] == 5120  # all 1023 coalitions at once
+    assert c.first_charac_fct_calls_count == 1023
+    v_all = c.charac_fct_values[tuple(range(10))]
+    assert abs(np.sum(c.contributivity_scores) - v_all) <= 1e-12 * max(1.0, abs(v_all))
+    vals = np.array([v for k, v in c.charac_fct_values.items() if k])
+    assert vals.min() > 0.5  # learnable data: every coalition learns (chance = 0.1)
+    # a partner's value grows with the data (all partners hold 10 %): the grand coalition beats singletons
+    assert v_all > np.mean([c.charac_fct_values[(i,)] for i in range(10)])
+
+
+def test_config3_batch_invariance(mnist10, config3_sweep):
+    c, eng = config3_sweep
+    for coal in [(3,), (2, 7), (0, 1, 4, 5, 8)]:
+        alone = eng.evaluate([coal])[0]
+        assert alone == c.charac_fct_values[coal], (coal, alone, c.charac_fct_values[coal])
+
+
+def test_config3_small_coalitions_vs_oracle(mnist10, config3_sweep):
+    from oracle import cnn as ocnn
+    c, eng = config3_sweep
+    ds = mnist10.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in mnist10.partners_list]
+    bs = [p.batch_size for p in mnist10.partners_list]
+    coals = [(3,), (6,), (8,), (2, 7), (0, 9), (4, 5)]
+    ref = np.array([ocnn.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
+    dev = np.array([c.charac_fct_values[k] for k in coals])
+    diff = np.abs(dev - ref)
+    assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
+
+
+# ------------------------------------------------------------------------------------------------
+# config #4
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cifar20():
+    from mplc.dataset import Cifar10
+    from mplc.scenario import Scenario
+    amounts = [0.05] * 19 + [float(1 - np.sum([0.05] * 19))]
+    sc = Scenario(20, amounts, dataset=Cifar10(synthetic=True, signal=0.4), minibatch_count=20,
+                  gradient_updates_per_pass_count=8, epoch_count=1, is_early_stopping=False)
+    return sc.provision()
+
+
+@pytest.fixture(scope="module")
+def config4_tmcs(cifar20):
+    from mplc.contributivity import Contributivity
+    np.random.seed(0)
+    c = Contributivity(scenario=cifar20)
+    c.compute_contributivity("TMCS")
+    return c
+
+
+def test_config4_tmcs_batched_equals_sequential_reference_loop(cifar20, config4_tmcs, monkeypatch):
+    """The batched / device-planned TMCS changes nothing: the reference's one-coalition-at-a-time loop fed
+    with the same v(S) values gives bit-identical scores, std, call count and memo order."""
+    import mplc.multi_partner_learning as mpl_mod
+    from mplc.contributivity import Contributivity
+    c = config4_tmcs
+    table = dict(cifar20.coalition_values)
+    table.update({k: v for k, v in c.charac_fct_values.items() if k})
+    calls = []
+
+    class TableMPL:  # the reference's plug-in protocol, one fit per coalition (mplc/contributivity.py:100-114)
+        def __init__(self, scenario, partners_list=None, partner=None, **kw):
+            if partner is not None:
+                partners_list = [partner]
+            self.ids = tuple(sorted(int(p.id) for p in partners_list))
+            self.history = types.SimpleNamespace(score=None)
+
+        def fit(self):
+            calls.append(self.ids)
+            self.history.score = table[self.ids]
+
+    monkeypatch.setattr(mpl_mod, "SinglePartnerLearning", TableMPL)
+    plain = types.SimpleNamespace(partners_list=cifar20.partners_list, multi_partner_learning_approach=TableMPL)
+    np.random.seed(0)
+    ref = Contributivity(scenario=plain)
+    ref.compute_contributivity("TMCS")
+    assert ref.name == c.name == "TMC Shapley"
+    assert np.array_equal(ref.contributivity_scores, c.contributivity_scores)
+    assert np.array_equal(ref.scores_std, c.scores_std)
+    assert ref.first_charac_fct_calls_count == c.first_charac_fct_calls_count == len(calls)
+    assert list(ref.charac_fct_values) == list(c.charac_fct_values)
+    assert c.first_charac_fct_calls_count > 100  # a real walk: many prefixes, truncation on
+    assert np.all(np.isfinite(c.contributivity_scores))
+
+
+def test_config4_coalitions_vs_oracle(cifar20, config4_tmcs):
+    from oracle import cifar_cnn as occ
+    c = config4_tmcs
+    eng = cifar20.engine
+    ds = cifar20.dataset
+    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in cifar20.partners_list]
+    bs = [p.batch_size for p in cifar20.partners_list]
+    coals = [(5,), (3, 11)]
+    dev = np.array([eng.evaluate([k])[0] for k in coals])
+    ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
+    diff = np.abs(dev - ref)
+    assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
