@@ -439,12 +439,14 @@ def bench_train(args, rank, world):
 # --------------------------------------------------------------------------------------------------
 # CIFAR10 TMCS/SMCS leg (config #4)
 # --------------------------------------------------------------------------------------------------
-def build_cifar_scenario(epochs, signal):
+def build_cifar_scenario(epochs, signal, partners=20):
     import numpy as np
     from mplc.dataset import Cifar10
     from mplc.scenario import Scenario
-    amounts = [0.05] * 19 + [float(1 - np.sum([0.05] * 19))]  # [0.05]*20 fails the reference's sum check
-    sc = Scenario(20, amounts, dataset=Cifar10(synthetic=True, signal=signal), minibatch_count=20,
+    # [0.05]*20 fails the reference's sum check: the last share is 1 - the others
+    amounts = [1.0 / partners] * (partners - 1)
+    amounts.append(float(1 - np.sum(amounts)))
+    sc = Scenario(partners, amounts, dataset=Cifar10(synthetic=True, signal=signal), minibatch_count=20,
                   gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False)
     return sc.provision()
 
@@ -479,7 +481,7 @@ def bench_cifar(args, rank, world):
     from mplc.contributivity import Contributivity
     from mplc.engine import CoalitionEngine
     from mplc.profiling import KernelTimer
-    sc = build_cifar_scenario(args.cifar_epochs, args.signal)
+    sc = build_cifar_scenario(args.cifar_epochs, args.signal, args.cifar_partners)
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
     eng.warmup()
@@ -520,10 +522,11 @@ def bench_cifar(args, rank, world):
         "steps": steps, "warmup": warm, "ms_per_step": round(wall * 1000 / steps, 1),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (CIFAR10-shaped: x = 0.4 class template + 0.6 U[0,1) fp32 [50000,32,32,3], one-hot labels)",
-        "config": {"workload": f"BASELINE config #4: CIFAR10 CNN, 20 partners, FedAvg, {args.method} (reference defaults, "
+        "config": {"workload": f"BASELINE config #4: CIFAR10 CNN, {args.cifar_partners} partners, FedAvg, {args.method} (reference defaults, "
                                f"numpy seed 0), E={args.cifar_epochs} fixed, M=20, G=8, coalitions LPT-sharded x{world}",
-                   "partners": 20, "method": args.method, "coalitions_evaluated": evals,
-                   "coalition_sizes": {str(k): sum(1 for c_ in coals if len(c_) == k) for k in range(1, 21)},
+                   "partners": args.cifar_partners, "method": args.method, "coalitions_evaluated": evals,
+                   "coalition_sizes": {str(k): sum(1 for c_ in coals if len(c_) == k)
+                                       for k in range(1, args.cifar_partners + 1)},
                    "train_samples_per_step_this_rank": int(samples / max(1, steps)),
                    "shapley_estimate": [round(float(v), 5) for v in c.contributivity_scores],
                    "replicas_per_launch": eng.stats.get("replicas", 0) / max(1, eng.stats.get("batches", 1)),
@@ -551,6 +554,7 @@ def main():
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
     ap.add_argument("--cifar-epochs", type=int, default=1)
+    ap.add_argument("--cifar-partners", type=int, default=20)
     ap.add_argument("--cifar-profile-kernel", default="conv2_fwd")
     ap.add_argument("--partners", type=int, default=10)
     ap.add_argument("--epochs", type=int, default=2)

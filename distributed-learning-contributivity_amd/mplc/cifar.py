@@ -63,6 +63,10 @@ class CifarModel:
     """Model hooks (see mplc.cnn.MnistModel) for the CIFAR10 CNN."""
     name = "cifar10_cnn"
     STRIDE, NPARAM = STRIDE, NPARAM
+    # Keras get_weights() order (mplc/dataset.py:170-190): (offset in a model row, shape)
+    KERAS_LAYERS = ((0, (3, 3, 3, 32)), (896, (32,)), (960, (3, 3, 32, 32)), (10176, (32,)), (10240, (3, 3, 32, 64)),
+                    (28672, (64,)), (28736, (3, 3, 64, 64)), (65600, (64,)), (65664, (2304, 512)), (1245312, (512,)),
+                    (1245824, (512, 10)), (1250944, (10,)))
     KERNEL_IDS = KERNEL_IDS
     input_shape = (32, 32, 3)
     # Keras 2.3.1 RMSprop(learning_rate=0.0001, decay=1e-6): rho 0.9, epsilon K.epsilon() = 1e-7

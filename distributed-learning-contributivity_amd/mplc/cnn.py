@@ -29,6 +29,17 @@ W2P = 18496
 WG_SAMPLES = 8
 PATIENCE = 10
 
+# Keras get_weights() order of the MNIST model (mplc/dataset.py:460-471): (offset in a model row, shape)
+KERAS_LAYERS = ((0, (3, 3, 1, 32)), (288, (32,)), (320, (3, 3, 32, 64)), (18752, (64,)), (18816, (9216, 128)),
+                (1198464, (128,)), (1198592, (128, 10)), (1199872, (10,)))
+
+
+def keras_weights(row, layers=KERAS_LAYERS):
+    """A model row (fp32, this engine's layout) as the list of arrays Keras' get_weights() returns."""
+    row = np.asarray(row, dtype=np.float32)
+    return [row[off:off + int(np.prod(shape))].reshape(shape).copy() for off, shape in layers]
+
+
 REP_IDLE, REP_FEDAVG, REP_SINGLE, REP_SEQ = -1, 0, 1, 2
 SEQ_REC = 6
 SEQ_APPROACHES = ("seq-pure", "seq-with-final-agg", "seqavg")
@@ -159,6 +170,7 @@ class MnistModel:
     workspaces, one lockstep step, evaluation.  TrainBatch / CnnBatchTrainer drive any model with these."""
     name = "mnist_cnn"
     STRIDE, NPARAM = STRIDE, NPARAM
+    KERAS_LAYERS = KERAS_LAYERS
     KERNEL_IDS = KERNEL_IDS
     input_shape = (28, 28)
 
@@ -438,7 +450,7 @@ class CnnBatchTrainer:
     def prepare(self, coalitions, epochs, record=False):
         return TrainBatch(self.eng, coalitions, epochs, self.lib, record=record)
 
-    def run(self, coalitions, epochs, early_stopping, history=None):
+    def run(self, coalitions, epochs, early_stopping, history=None, keep_models=False):
         """Train the coalitions in lockstep; returns (test accuracies, epochs done).  With `history` (a
         dict, one coalition only) the learning history is recorded into it (HistoryRecorder)."""
         eng = self.eng
@@ -506,6 +518,7 @@ class CnnBatchTrainer:
             rec.finish(epochs_done[0])
         glob = st.finalize()
         self.last_es_trace = val_hist
+        self.last_models = glob.cpu().numpy() if keep_models else None
         correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
         return correct / float(eng.y_test_d.numel()), epochs_done
 

@@ -145,6 +145,22 @@ class Contributivity:
             for k, v in zip(todo, values):
                 cache[k] = float(v)
 
+    def _world_size(self):
+        from .parallel import world
+        return world()[1]
+
+    def _lookahead(self, per_iteration):
+        """Sampling iterations to plan ahead so that one planned batch holds about `mc_plan_coalitions`
+        (default 512) coalitions per rank - several hundred replicas per GPU launch (SMCS batches
+        of <= 2N coalitions left the GPU idle).  Speculation never changes a result: v(S) is a deterministic
+        function of (S, seed), planning restores the RNG state, and draws that the real loop does not make
+        only cost compute."""
+        target = int(getattr(self.scenario, "mc_plan_coalitions", 512)) * self._world_size()
+        return max(1, target // max(1, per_iteration))
+
+    def _known(self, key):
+        return key in self.charac_fct_values or key in self._cache()
+
     def _coalition_value(self, key):
         cache = self._cache()
         if key in cache:
@@ -308,7 +324,10 @@ class Contributivity:
         sizes = self._sizes()
         while t < 100 or t < q ** 2 * v_max / sv_accuracy ** 2:
             if t >= wave:
-                span = 100 if t < 100 else 50
+                # waves grow with the world size so that every rank's frontier batches stay as large as one
+                # GPU's (mc_wave_scale overrides); more permutations per wave only adds speculation
+                scale = int(getattr(self.scenario, "mc_wave_scale", 0) or self._world_size())
+                span = (100 if t < 100 else 50) * scale
                 self._prefetch_permutation_wave(n, v_all, truncation, span, interpolate, sizes)
                 wave = t + span
             t += 1
@@ -387,23 +406,18 @@ class Contributivity:
         t = 0
         v_max = 0
         S = None
+        planned_until = 0
         while t < 100 or t < 4 * q ** 2 * v_max / sv_accuracy ** 2:
             t += 1
             if t > rows.shape[0]:
                 rows = np.vstack((rows, np.zeros_like(rows)))
             rows[t - 1] = 0.0
-            # plan this iteration's draws on a copy of the RNG, batch the needed coalitions
-            if self._batched_evaluator() is not None:
-                state = np.random.get_state()
-                plan = []
-                for k in range(n):
-                    u = np.random.uniform(0, 1, 1)[0]
-                    idx = _first_index_above(tables[k][1], u)
-                    if idx is not None:
-                        sub = tables[k][0][idx]
-                        plan += [tuple(sorted(sub + (k,))), sub]
-                np.random.set_state(state)
-                self.prefetch(plan)
+            # the sampling tables are fixed for the whole loop, so the draws of the next iterations are known
+            # exactly: plan several iterations on a copy of the RNG state, batch the coalitions they need
+            if self._batched_evaluator() is not None and t > planned_until:
+                K = self._lookahead(2 * n)
+                self.prefetch(self._plan_importance(n, tables, K, S))
+                planned_until = t + K - 1
             for k in range(n):
                 u = np.random.uniform(0, 1, 1)[0]
                 idx = _first_index_above(tables[k][1], u)
@@ -417,6 +431,24 @@ class Contributivity:
             v_max = np.max(np.var(rows[:t], axis=0))
         contributions = rows[:t]
         return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1)
+
+    @staticmethod
+    def _plan_importance(n, tables, iterations, S):
+        """Coalitions the importance-sampling loop will ask for in its next `iterations` iterations (one
+        uniform per player per iteration, mplc/contributivity.py:405-431), drawn from a saved RNG state."""
+        state = np.random.get_state()
+        plan = []
+        cur = None if S is None else tuple(int(i) for i in S)
+        for _ in range(iterations):
+            for k in range(n):
+                idx = _first_index_above(tables[k][1], np.random.uniform(0, 1, 1)[0])
+                if idx is not None:
+                    cur = tables[k][0][idx]
+                if cur is None:
+                    break
+                plan += [tuple(sorted(cur + (k,))), cur]
+        np.random.set_state(state)
+        return plan
 
     def IS_lin(self, sv_accuracy=0.01, alpha=0.95):
         self._begin()
@@ -557,6 +589,7 @@ class Contributivity:
         contributions = None
         S = None
         j = 0
+        planned_until = 0
         while t < 100 or t < 4 * q ** 2 * v_max / sv_accuracy ** 2:
             if t == 0:
                 contributions = np.array([np.zeros(n)])
@@ -578,15 +611,11 @@ class Contributivity:
                 tables, renorms = self._importance_tables(n, approx_for)
                 gen_tables.append((tables, renorms, approx_for))
             tables, renorms, approx_for = gen_tables[j]
-            if self._batched_evaluator() is not None:
-                state = np.random.get_state()
-                plan = []
-                for k in range(n):
-                    idx = _first_index_above(tables[k][1], np.random.uniform(0, 1, 1)[0])
-                    if idx is not None:
-                        plan += [tuple(sorted(tables[k][0][idx] + (k,))), tables[k][0][idx]]
-                np.random.set_state(state)
-                self.prefetch(plan)
+            if self._batched_evaluator() is not None and t >= planned_until:
+                # exact up to the next refit (the tables of this generation are fixed until then)
+                K = min(self._lookahead(2 * n), update - t % update)
+                self.prefetch(self._plan_importance(n, tables, K, S))
+                planned_until = t + K
             for k in range(n):
                 u = np.random.uniform(0, 1, 1)[0]
                 idx = _first_index_above(tables[k][1], u)
@@ -662,26 +691,53 @@ class Contributivity:
         samples = [[[] for _ in range(N)] for _ in range(N)]
         S = None
         var = np.zeros(N)
-        while np.any(keep_going) or (1 - alpha) < v_max / (sv_accuracy ** 2):
-            t += 1
-            e = 1 + 1 / (1 + np.exp(gamma / beta)) - 1 / (1 + np.exp(-(t - gamma * N) / (beta * N)))
+        planned_until = 0
 
-            def alloc(k):
-                if np.sum(sigma2[k]) == 0:
-                    return np.repeat(1 / N, N)
-                return np.repeat(1 / N, N) * (1 - e) + sigma2[k] / np.sum(sigma2[k]) * e
+        def exploration(t):
+            return 1 + 1 / (1 + np.exp(gamma / beta)) - 1 / (1 + np.exp(-(t - gamma * N) / (beta * N)))
 
-            # within one iteration the draws of player k depend only on sigma2[k] from earlier iterations
-            if self._batched_evaluator() is not None:
-                state = np.random.get_state()
-                plan = []
+        def allocation(k, e):
+            if np.sum(sigma2[k]) == 0:
+                return np.repeat(1 / N, N)
+            return np.repeat(1 / N, N) * (1 - e) + sigma2[k] / np.sum(sigma2[k]) * e
+
+        def plan(t0, iterations):
+            """Draws of iterations t0, t0+1, ... from a saved RNG state with sigma2 as it stands.  Every draw
+            consumes one uniform (np.random.choice with p) plus one (the subset), whatever the values, so
+            the stream stays aligned; within iteration t0 the plan is exact (player k's allocation only
+            depends on sigma2[k] from earlier iterations), later ones speculate that sigma2 does not move
+            the stratum draw (after the first ~gamma*N iterations the exploration weight e is ~1e-12)."""
+            state = np.random.get_state()
+            out = []
+            cur = S
+            for tt in range(t0, t0 + iterations):
+                e_t = exploration(tt)
                 for k in range(N):
-                    st = np.random.choice(np.arange(N), 1, p=alloc(k))[0]
+                    st = np.random.choice(np.arange(N), 1, p=allocation(k, e_t))[0]
                     sub = self._stratified_pick(N, k, st, np.random.uniform(0, 1, 1)[0])
                     if sub is not None:
-                        plan += [tuple(sorted(sub + (k,))), sub]
-                np.random.set_state(state)
-                self.prefetch(plan)
+                        cur = sub
+                    if cur is not None:
+                        cur = tuple(int(i) for i in cur)
+                        out += [tuple(sorted(cur + (k,))), cur]
+            np.random.set_state(state)
+            return out
+
+        while np.any(keep_going) or (1 - alpha) < v_max / (sv_accuracy ** 2):
+            t += 1
+            e = exploration(t)
+
+            def alloc(k):
+                return allocation(k, e)
+
+            if self._batched_evaluator() is not None:
+                exact = plan(t, 1)
+                if t > planned_until or not all(self._known(c) for c in exact):
+                    # speculate only once the allocation has settled (e ~ 0): before that, each iteration
+                    # is planned exactly on its own
+                    K = self._lookahead(2 * N) if t > gamma * N + 8 else 1
+                    self.prefetch(exact + (plan(t + 1, K - 1) if K > 1 else []))
+                    planned_until = t + K - 1
             for k in range(N):
                 strata = np.random.choice(np.arange(N), 1, p=alloc(k))[0]
                 u = np.random.uniform(0, 1, 1)[0]
@@ -710,6 +766,50 @@ class Contributivity:
             v_max = np.max(var)
         self._finish("Stratified MC Shapley", shap, np.sqrt(var))
 
+    @staticmethod
+    def _plan_wr_smc(N, iterations, keep_going, sigma2, drawn, pending):
+        """Draws of the next `iterations` WR_SMC iterations (mplc/contributivity.py:858-900) from a saved RNG
+        state.  The without-replacement bookkeeping is simulated exactly (pops from the pending lists, draw
+        counts, the keep_going flags they switch off); once every stratum of a player is done the allocation
+        follows sigma2, taken as it stands (speculation).  Pending lists are not copied (2^(N-1) entries per
+        player at N=20): simulated pops are an overlay of removed positions."""
+        state = np.random.get_state()
+        out = []
+        counts = [[len(drawn[k][s]) for s in range(N)] for k in range(N)]
+        keep = [list(row) for row in keep_going]
+        removed = {}
+        full = [[len(pending[k][s]) + len(drawn[k][s]) for s in range(N)] for k in range(N)]
+        for _ in range(iterations):
+            for k in range(N):
+                if np.any(keep[k]):
+                    p = np.array(keep[k]) / np.sum(keep[k])
+                elif np.sum(sigma2[k]) == 0:
+                    continue
+                else:
+                    p = sigma2[k] / np.sum(sigma2[k])
+                st = np.random.choice(np.arange(N), 1, p=p)[0]
+                gone = removed.setdefault((k, st), [])
+                L = len(pending[k][st]) - len(gone)
+                if L <= 0:  # speculation ran into an exhausted stratum: stop planning here
+                    np.random.set_state(state)
+                    return out
+                pick = np.random.choice(L, 1, p=np.repeat(1 / L, L))[0]
+                # position `pick` of the list after the simulated pops -> position in the real list
+                i = int(pick)
+                for g in sorted(gone):
+                    if g <= i:
+                        i += 1
+                gone.append(i)
+                sub = tuple(int(v) for v in pending[k][st][i])
+                out += [tuple(sorted(sub + (k,))), sub]
+                counts[k][st] += 1
+            for k in range(N):
+                for s in range(N):
+                    if counts[k][s] > 20 or counts[k][s] == full[k][s]:
+                        keep[k][s] = False
+        np.random.set_state(state)
+        return out
+
     def without_replacment_SMC(self, sv_accuracy=0.01, alpha=0.95):
         self._begin()
         N = self._n
@@ -727,6 +827,7 @@ class Contributivity:
             others = [i for i in range(N) if i != k]
             pending.append([list(combinations(others, strata)) for strata in range(N)])
         var = np.zeros(N)
+        planned_until = 0
         while np.any(keep_going) or (1 - alpha) < v_max / (sv_accuracy ** 2):
             t += 1
 
@@ -738,18 +839,11 @@ class Contributivity:
                 return sigma2[k] / np.sum(sigma2[k])
 
             if self._batched_evaluator() is not None:
-                state = np.random.get_state()
-                plan = []
-                for k in range(N):
-                    p = alloc(k)
-                    if p is None:
-                        continue
-                    st = np.random.choice(np.arange(N), 1, p=p)[0]
-                    L = len(pending[k][st])
-                    sub = pending[k][st][np.random.choice(L, 1, p=np.repeat(1 / L, L))[0]]
-                    plan += [tuple(sorted(sub + (k,))), sub]
-                np.random.set_state(state)
-                self.prefetch(plan)
+                exact = self._plan_wr_smc(N, 1, keep_going, sigma2, drawn, pending)
+                if t > planned_until or not all(self._known(c) for c in exact):
+                    K = self._lookahead(2 * N)
+                    self.prefetch(self._plan_wr_smc(N, K, keep_going, sigma2, drawn, pending))
+                    planned_until = t + K - 1
             for k in range(N):
                 p = alloc(k)
                 if p is None:

@@ -171,9 +171,10 @@ class CoalitionEngine:
     supports_history = True
 
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
-                 record_history=False):
+                 record_history=False, return_models=False):
         """v(S) (test accuracy, float64) for each coalition (sorted tuple of partner indices).  With
-        record_history (one coalition) the details also hold its learning history (cnn.HistoryRecorder)."""
+        record_history (one coalition) the details also hold its learning history (cnn.HistoryRecorder);
+        with return_models, the final models as Keras get_weights() lists (details["models"])."""
         coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
         for c in coalitions:
             if len(c) == 0 or c[0] < 0 or c[-1] >= len(self.partner_sizes) or len(set(c)) != len(c):
@@ -183,6 +184,7 @@ class CoalitionEngine:
         scores = np.zeros(len(coalitions))
         epochs_done = np.zeros(len(coalitions), dtype=np.int64)
         es_trace = [[] for _ in coalitions]
+        models = [None] * len(coalitions)
         history = None
         if record_history:
             if len(coalitions) != 1:
@@ -190,11 +192,15 @@ class CoalitionEngine:
             history = {}
         for batch in self.plan_batches(coalitions):
             coal = [coalitions[i] for i in batch]
-            s, e = self.trainer.run(coal, E, es, history=history)
+            s, e = self.trainer.run(coal, E, es, history=history, keep_models=return_models)
             scores[batch] = s
             epochs_done[batch] = e
             for i, tr in zip(batch, getattr(self.trainer, "last_es_trace", [[]] * len(batch))):
                 es_trace[i] = list(tr)
+            if return_models:
+                from .cnn import keras_weights
+                for j, i in enumerate(batch):
+                    models[i] = keras_weights(self.trainer.last_models[j], self.model_impl.KERAS_LAYERS)
             self.stats["batches"] += 1
             self.stats["replicas"] += sum(len(c) for c in coal)
             # samples trained (every replica sees all its partner's rows once per epoch done)
@@ -205,6 +211,8 @@ class CoalitionEngine:
             # es_val_loss: the val losses the early-stopping rule compared (start-of-epoch global model for
             # FedAvg, end-of-epoch model for singletons); empty when early stopping is inactive
             out = {"scores": scores, "epochs_done": epochs_done, "es_val_loss": es_trace}
+            if return_models:
+                out["models"] = models
             if history is not None:
                 out["history"] = history
             return out

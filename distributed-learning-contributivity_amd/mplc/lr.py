@@ -58,7 +58,7 @@ class LogRegEngine:
     HIST_BLOCK = 2 + 4 * MAXP
 
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
-                 record_history=False):
+                 record_history=False, return_models=False):
         """v(S) for each coalition; with record_history (one coalition) the details also hold its learning
         history (mplc/mpl_utils.py:11-27) in the layout of multi_partner_learning.History."""
         import torch
@@ -113,6 +113,8 @@ class LogRegEngine:
         self.stats["replicas"] += sum(len(c) for c in coalitions)
         if return_details:
             out = {"scores": scores, "epochs_done": epochs_done.cpu().numpy().astype(np.int64)}
+            if return_models:  # Titanic.LogisticRegression.get_weights(): [coef | intercept], shape (1, 28)
+                out["models"] = [self.last_theta[ci].reshape(1, -1).copy() for ci in range(C)]
             if hist is not None:
                 out["history"] = self._history(coalitions[0], hist.cpu().numpy().reshape(E, M, self.HIST_BLOCK))
             return out

@@ -108,6 +108,10 @@ class MultiPartnerLearning:
         eng = _engine(self.scenario)
         record = self.record_history and getattr(eng, "supports_history", False)
         kw = dict(record_history=True) if record else {}
+        # a dry-run scenario writes nothing (the reference's is_dry_run skips the experiment folder)
+        save = self.is_save_data and self.save_folder is not None and not getattr(self.scenario, "is_dry_run", False)
+        if save:
+            kw["return_models"] = True
         res = eng.evaluate([self._coalition()], epoch_count=self.epoch_count,
                            is_early_stopping=self.is_early_stopping, return_details=True, **kw)
         self.history.score = float(res["scores"][0])
@@ -115,7 +119,29 @@ class MultiPartnerLearning:
         if record:  # keyed by partner.id (== the engine's partner index) and 'mpl_model'
             self.history.history = res["history"]
             self.epoch_index = self.history.nb_epochs_done - 1
+        if save:
+            self.model_weights = res["models"][0]
+            self.save_final_model()
         self.learning_computation_time = timer() - start
+
+    def save_final_model(self):
+        """mplc/multi_partner_learning.py:117-128: <save_folder>/model/<dataset>_final_weights.npy, the final
+        model's get_weights() list saved with np.save (an object array, as the reference writes it).  The
+        reference saves after EVERY fit - each coalition of a contributivity run overwrites the same file, so
+        what survives is an arbitrary coalition's model; here the learners that save are the ones built with
+        is_save_data=True (Scenario.run's main fit), so the file holds the grand coalition's final model.
+        The Keras .h5 copy is not written: h5py / Keras are not available."""
+        import os
+        folder = os.path.join(str(self.save_folder), "model")
+        os.makedirs(folder, exist_ok=True)
+        name = getattr(self.dataset, "name", "model")
+        w = self.model_weights
+        if isinstance(w, np.ndarray):  # Titanic LR: one (1, 28) array
+            np.save(os.path.join(folder, name + "_final_weights.npy"), w)
+            return
+        arr = np.empty(len(w), dtype=object)
+        arr[:] = list(w)
+        np.save(os.path.join(folder, name + "_final_weights.npy"), arr, allow_pickle=True)
 
     # Contributivity plans TMCS/ITMCS permutation waves with the device walk (mplc.mc) for this approach
     device_planning = True

@@ -110,6 +110,7 @@ class Scenario:
         self.scenario_name = f"scenario_{scenario_id}_repeat_{self.n_repeat}_{now}_{uuid.uuid4().hex[:3]}"
         self.short_scenario_name = f"{self.partners_count} {self.amounts_per_partner}"
         self.save_folder = Path(experiment_path) / self.scenario_name
+        self.is_dry_run = is_dry_run
         if not is_dry_run:
             self.save_folder.mkdir(parents=True, exist_ok=True)
         self.engine = None

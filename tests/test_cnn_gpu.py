@@ -287,3 +287,28 @@ def test_early_stopping_matches_reference_rule_and_oracle():
         assert np.allclose(trace[:3], ref_trace[:3], rtol=5e-2, atol=0), (c, trace[:3], ref_trace[:3])
         assert abs(int(res["epochs_done"][i]) - ref_ep) <= 3, (c, res["epochs_done"][i], ref_ep)
         assert abs(res["scores"][i] - ref_acc) <= 0.03, (c, res["scores"][i], ref_acc)
+
+
+def test_scenario_run_saves_final_model(tmp_path):
+    """save_final_model (mplc/multi_partner_learning.py:117-128): Scenario.run's main fit writes
+    <save_folder>/model/mnist_final_weights.npy, the get_weights() list of the final model (Keras shapes);
+    that model, evaluated by the oracle, scores the run's mpl_test_score."""
+    from mplc.dataset import ArrayDataset, digits_as_mnist
+    from mplc.scenario import Scenario
+    x, y = digits_as_mnist()
+    ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:])
+    sc = Scenario(3, [0.2, 0.5, 0.3], dataset=ds, minibatch_count=2, gradient_updates_per_pass_count=4,
+                  epoch_count=2, is_early_stopping=False, experiment_path=tmp_path, is_dry_run=False)
+    sc.run()
+    f = sc.save_folder / "model" / "mnist_final_weights.npy"
+    assert f.exists()
+    w = np.load(f, allow_pickle=True)  # our own file: the reference's object-array format
+    shapes = [(3, 3, 1, 32), (32,), (3, 3, 32, 64), (64,), (9216, 128), (128,), (128, 10), (10,)]
+    assert [a.shape for a in w] == shapes and all(a.dtype == np.float32 for a in w)
+    row = np.zeros(ocnn.STRIDE, dtype=np.float32)
+    for (name, (off, shape)), a in zip(ocnn.OFF.items(), w):
+        row[off:off + a.size] = a.reshape(-1)
+    data = ocnn.Data(sc.dataset.x_train, sc.dataset.y_train, sc.dataset.x_val, sc.dataset.y_val,
+                     sc.dataset.x_test, sc.dataset.y_test)
+    _, acc = ocnn.evaluate(ocnn.unpack(row), data.x_test, data.y_test)
+    assert abs(acc - sc.mpl.history.score) <= 1 / len(data.y_test) + 1e-12, (acc, sc.mpl.history.score)

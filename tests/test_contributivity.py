@@ -150,3 +150,26 @@ def test_exact_shapley_on_device_matches_reference(case, monkeypatch):
     assert c.first_charac_fct_calls_count == case["calls_count"]
     assert [list(x) for x in calls] == case["fit_order"]
     assert nxt == case["rng_next_uniform"]
+
+
+@pytest.mark.parametrize("method,n,max_batches", [("SMCS", 10, 40), ("SMCS", 8, 30), ("WR_SMC", 8, 10),
+                                                  ("IS_lin_S", 8, 15)])
+def test_speculative_planning_makes_few_large_batches(method, n, max_batches, monkeypatch):
+    """SMCS / WR_SMC / IS plan several iterations ahead (one iteration = at most 2N coalitions per
+    launch): the whole estimator needs only a few engine batches, and still matches the reference."""
+    case = next(c for c in CASES if c["method"] == method and c["n"] == n and not c["error"])
+    calls, batches = [], []
+    scenario, fake = make_scenario(case, calls, batched=True)
+    inner = fake.evaluate_coalitions
+
+    def counting(sc, coalitions):
+        batches.append(len(coalitions))
+        return inner(sc, coalitions)
+    fake.evaluate_coalitions = staticmethod(counting)
+    monkeypatch.setattr(mpl_mod, "SinglePartnerLearning", fake)
+    np.random.seed(case["seed"])
+    c = Contributivity(scenario=scenario)
+    c.compute_contributivity(method)
+    assert same(np.atleast_1d(c.contributivity_scores), case["scores"])
+    assert c.first_charac_fct_calls_count == case["calls_count"]
+    assert len(batches) <= max_batches, batches

@@ -28,6 +28,40 @@ def test_lpt_shard_balanced_and_complete():
         assert max(loads) - min(loads) <= max(costs)
 
 
+def _table(n=6):
+    from itertools import combinations
+    sizes = [30 + 10 * i for i in range(n)]
+    rng = np.random.default_rng(1)
+    table = {}
+    for r in range(1, n + 1):
+        for c in combinations(range(n), r):
+            table[c] = float(sum(sizes[i] for i in c)) / sum(sizes) + 0.01 * rng.uniform()
+    return sizes, table
+
+
+def _sequential_reference(method, seed, monkeypatch):
+    """The estimator the reference's way: one fit per coalition, no planning, one process."""
+    import types
+    import mplc.multi_partner_learning as mpl_mod
+    from mplc.contributivity import Contributivity
+    sizes, table = _table()
+
+    class TableMPL:
+        def __init__(self, scenario, partners_list=None, partner=None, **kw):
+            self.ids = tuple(sorted(int(p.id) for p in ([partner] if partner is not None else partners_list)))
+            self.history = types.SimpleNamespace(score=None)
+
+        def fit(self):
+            self.history.score = table[self.ids]
+    monkeypatch.setattr(mpl_mod, "SinglePartnerLearning", TableMPL)
+    partners = [types.SimpleNamespace(id=i, y_train=np.zeros(s)) for i, s in enumerate(sizes)]
+    sc = types.SimpleNamespace(partners_list=partners, multi_partner_learning_approach=TableMPL)
+    np.random.seed(seed)
+    c = Contributivity(scenario=sc)
+    c.compute_contributivity(method)
+    return c
+
+
 def _worker(rank, world, port, out_q):
     import sys
     import types
@@ -40,14 +74,7 @@ def _worker(rank, world, port, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mplc.parallel import sharded_evaluate
     from mplc.contributivity import Contributivity
-    n = 6
-    sizes = [30 + 10 * i for i in range(n)]
-    rng = np.random.default_rng(1)
-    table = {}
-    from itertools import combinations
-    for r in range(1, n + 1):
-        for c in combinations(range(n), r):
-            table[c] = float(sum(sizes[i] for i in c)) / sum(sizes) + 0.01 * rng.uniform()
+    sizes, table = _table()
     seen = []
 
     def local(coals):
@@ -66,15 +93,19 @@ def _worker(rank, world, port, out_q):
 
     partners = [types.SimpleNamespace(id=i, y_train=np.zeros(s)) for i, s in enumerate(sizes)]
     sc = types.SimpleNamespace(partners_list=partners, multi_partner_learning_approach=Approach)
-    np.random.seed(7)
-    c = Contributivity(scenario=sc)
-    c.compute_contributivity("TMCS")
-    out_q.put((rank, mine, c.contributivity_scores.tolist(), c.first_charac_fct_calls_count))
+    results = {}
+    for method in ("TMCS", "SMCS"):
+        # world size 2: TMCS waves are twice as long, SMCS plans twice as many iterations ahead
+        np.random.seed(7)
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity(method)
+        results[method] = (c.contributivity_scores.tolist(), c.scores_std.tolist(), c.first_charac_fct_calls_count)
+    out_q.put((rank, mine, results))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_evaluation_and_spmd_estimator():
+def test_two_rank_sharded_evaluation_and_spmd_estimator(monkeypatch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -85,8 +116,15 @@ def test_two_rank_sharded_evaluation_and_spmd_estimator():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
+    res.sort(key=lambda r: r[0])
     # each rank trained only part of the coalitions (shards partition the 63 coalitions ...)
     assert res[0][1] > 0 and res[1][1] > 0
-    # ... and both ranks computed identical estimates and memo semantics
-    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]
+    # ... both ranks computed identical estimates and memo semantics ...
+    assert res[0][2] == res[1][2]
+    # ... equal, bit for bit, to the sequential single-process reference loop (larger speculative waves and
+    # deeper SMCS planning at world size 2 change nothing)
+    for method in ("TMCS", "SMCS"):
+        ref = _sequential_reference(method, 7, monkeypatch)
+        scores, std, calls = res[0][2][method]
+        assert scores == ref.contributivity_scores.tolist() and std == ref.scores_std.tolist(), method
+        assert calls == ref.first_charac_fct_calls_count, method
