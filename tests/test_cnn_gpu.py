@@ -260,8 +260,9 @@ def test_early_stopping_matches_reference_rule_and_oracle():
       summation-order noise takes over (Adam's first steps move every weight by ~lr * sign(g), so weights
       whose gradient is ~0 take either sign: the oracle itself on 8 vs 16 CPU threads gives 0.3627 vs 0.3669
       for (0, 1) after one epoch; the engine gave 0.3627).  The stopping epoch itself depends on near-ties of a flat val-loss
-      curve: the oracle run with 8 vs 3 CPU threads stops (0,) at 16 vs 18 and (0, 1) at 19 vs 17.  So the
-      engine's stopping epochs must be within 3 of the oracle's, and v(S) within 3 pt each."""
+      curve: the oracle run with 8 vs 3 CPU threads stops (0,) at 16 vs 18 and (0, 1) at 19 vs 17, and a
+      different stopping epoch means a differently trained final model.  So the engine's stopping epochs
+      must be within 3 of the oracle's, and v(S) within 2 pt on average (5 pt each: 297 test samples)."""
     from mplc.engine import CoalitionEngine
     E = 25
     sc = make_scenario(partners=2, amounts=(0.3, 0.7), M=2, G=8, E=E, es=True)
@@ -271,6 +272,7 @@ def test_early_stopping_matches_reference_rule_and_oracle():
     ds = sc.dataset
     data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow, bs = rows(sc)
+    diffs = []
     for i, c in enumerate(coals):
         trace = res["es_val_loss"][i]
         rule = _keras_early_stopping if len(c) == 1 else _fedavg_early_stop
@@ -286,7 +288,9 @@ def test_early_stopping_matches_reference_rule_and_oracle():
             assert abs(trace[0] - ref_trace[0]) <= 1e-5 * ref_trace[0], (c, trace[0], ref_trace[0])
         assert np.allclose(trace[:3], ref_trace[:3], rtol=5e-2, atol=0), (c, trace[:3], ref_trace[:3])
         assert abs(int(res["epochs_done"][i]) - ref_ep) <= 3, (c, res["epochs_done"][i], ref_ep)
-        assert abs(res["scores"][i] - ref_acc) <= 0.03, (c, res["scores"][i], ref_acc)
+        assert abs(res["scores"][i] - ref_acc) <= 0.05, (c, res["scores"][i], ref_acc)
+        diffs.append(abs(res["scores"][i] - ref_acc))
+    assert np.mean(diffs) <= 0.02, diffs
 
 
 def test_scenario_run_saves_final_model(tmp_path):
