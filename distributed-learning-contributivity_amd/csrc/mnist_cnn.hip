@@ -89,6 +89,18 @@ __device__ __forceinline__ floatx16 conv1_mfma(const float* img_s, int pix, int 
   return acc;
 }
 
+// XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one,
+// MI355X_MICROARCH.md), so a replica's consecutive blocks would land on all 8 XCDs and each XCD's L2 would
+// fetch that replica's weights.  The flat block id is remapped so that each XCD walks a contiguous range of
+// logical blocks (replica-major): the blocks of one replica share an XCD and its L2.  The mapping only
+// permutes which workgroup does which tile of work; every result is bit-identical.
+__device__ __forceinline__ int64_t xcd_block() {
+  const int64_t n = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+  const int64_t b = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+  const int64_t q = n / 8;
+  return b < 8 * q ? (b % 8) * q + b / 8 : b;
+}
+
 // accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
 __device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
 
@@ -170,9 +182,10 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     uint8_t* __restrict__ code) {
   __shared__ float img_s[FWD_IMR * IMG];
   __shared__ float a1_s[FWD_C1R * A1 * A1P];
-  const int part = blockIdx.x;
-  const int j = blockIdx.y;
-  const int r = blockIdx.z;
+  const int64_t lb = xcd_block();  // logical block (part, j, r), replica-major
+  const int part = (int)(lb % FWD_PARTS);
+  const int j = (int)((lb / FWD_PARTS) % gridDim.y);
+  const int r = (int)(lb / ((int64_t)FWD_PARTS * gridDim.y));
   const int count = cnt ? cnt[r] : cnt_all;
   if (j >= count) return;
   const int tid = threadIdx.x;
@@ -501,8 +514,9 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     float* __restrict__ adam_v, int64_t stride, float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
   __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
   __shared__ float p_s[D1_SCHUNK * D1_ROWS];
-  const int r = blockIdx.y;
-  const int k0 = blockIdx.x * D1_ROWS;
+  const int64_t lb = xcd_block();  // logical block (slice, r), replica-major: dh and p stay in one L2
+  const int r = (int)(lb / gridDim.x);
+  const int k0 = (int)(lb % gridDim.x) * D1_ROWS;
   const int count = cnt[r];
   if (count == 0) return;
   const int tid = threadIdx.x;
@@ -593,7 +607,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     __builtin_nontemporal_store(mv[i], Mr + 8 * i);
     __builtin_nontemporal_store(vv[i], Vr + 8 * i);
   }
-  if (blockIdx.x == 0 && tid < HID) {
+  if (k0 == 0 && tid < HID) {  // the replica's slice-0 block (logical order)
     float gb = 0.0f;
     const float* dHs = dH + (int64_t)r * bmax * HID;
     for (int jj = 0; jj < count; ++jj) gb += dHs[(int64_t)jj * HID + tid];
@@ -663,9 +677,10 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   __shared__ float dz_s[DZR * DZC * DZQ];
   __shared__ float img_s[(BAND + 2) * IMG];
   __shared__ float red_s[4][10 * 32];
-  const int band = blockIdx.x & 1;
-  const int j = blockIdx.x >> 1;
-  const int r = blockIdx.y;
+  const int64_t lb = xcd_block();  // logical block (band, j, r), replica-major
+  const int band = (int)(lb & 1);
+  const int j = (int)((lb % gridDim.x) >> 1);
+  const int r = (int)(lb / gridDim.x);
   if (j >= cnt[r]) return;
   const int tid = threadIdx.x;
   const int row = idx[(int64_t)r * bmax + j];
