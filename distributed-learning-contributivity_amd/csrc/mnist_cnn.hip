@@ -161,12 +161,60 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv1 (recompute) + conv2 (MFMA) + bias + ReLU + 2x2 max-pool.  Block = (third of the image: 4 pool rows,
-// slot, model), 4 waves - one per SIMD, so the block's MFMA work is spread evenly over the CU.  6 row tiles
-// x 2 channel tiles of 32x32; wave w owns channel tile w & 1 of row tiles 3 (w >> 1) .. +2.  A row tile =
-// 8 pooling windows x 4 pixels, laid out so that the 4 pixels of a window are accumulator registers
-// 4g..4g+3 of one lane: the pool is a register max.  A third needs 10 conv1 rows (34 KB of LDS): four
-// blocks share a CU.
+// conv2 in Winograd form F(2x2, 3x3) (Lavin & Gray): per 4x4 input patch d and 3x3 kernel g,
+//   Y[2x2] = A^T [ (G g G^T) (.) (B^T d B) ] A,   with one output tile = one 2x2 max-pool window.
+// W2 is transformed once per model and step: U[xi = 4i + j][ci][co] = (G g G^T)[i][j] (winograd_w2_kernel).
+// The conv becomes 16 independent GEMMs M[xi][tile][co] = sum_ci V[xi][tile][ci] U[xi][ci][co]: 2.25x fewer
+// multiply-adds than the direct convolution (16 x 32 x 64 per tile of 4 outputs instead of 4 x 288 x 64).
+// All arithmetic stays fp32 (the transforms are sums, differences and halvings; MFMA accumulation is f32).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) {  // o = G g (one column)
+  o[0] = g[0];
+  o[1] = 0.5f * ((g[0] + g[1]) + g[2]);
+  o[2] = 0.5f * ((g[0] - g[1]) + g[2]);
+  o[3] = g[2];
+}
+
+__global__ __launch_bounds__(256) void winograd_w2_kernel(const float* __restrict__ params, int64_t stride,
+                                                          const int32_t* __restrict__ cnt, float* __restrict__ U) {
+  const int r = blockIdx.y;
+  if (cnt && cnt[r] == 0) return;
+  const int e = blockIdx.x * 256 + threadIdx.x;  // (ci, co)
+  if (e >= C1 * C2) return;
+  const float* W2 = params + (int64_t)r * stride + OFF_W2 + e;  // [kyx][ci][co]: tap k at W2[k * C1 * C2]
+  float g[3][3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) g[ky][kx] = W2[(ky * 3 + kx) * C1 * C2];
+  float gg[4][3];  // G g: rows i, columns kx
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const float col[3] = {g[0][kx], g[1][kx], g[2][kx]};
+    float o[4];
+    wino_g_rows(col, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
+  }
+  float* Ur = U + (int64_t)r * MPLC_CNN_W2T + e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float o[4];
+    wino_g_rows(gg[i], o);  // (G g) G^T: row i
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) Ur[(4 * i + jj) * C1 * C2] = o[jj];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// conv1 (recompute) + conv2 (Winograd, MFMA) + bias + ReLU + 2x2 max-pool.  Block = (third of the image:
+// 4 pool rows = 48 tiles, slot, model), 4 waves.  Wave i owns transform row i (xi = 4i .. 4i+3) of the three
+// 16-tile groups x 4 channel groups: 48 accumulators of v_mfma_f32_16x16x4_f32 (tile x co), K = 32 input
+// channels in 8 steps of 4.  A operands (V) are computed in registers from the LDS conv1 tile (8 reads and
+// 8 adds give a lane its 4 values of V for one (tile, ci)); B operands (U, L2-resident) are loaded one
+// k-step ahead.  Output: each wave folds its row of the output transform (T_i = M_i A, 2 values per
+// (tile, co)) into LDS; then Y = sum_i A^T[.][i] T_i + bias, the max over the window (first max in scan
+// order) and ReLU, written with the argmax code.
 // ------------------------------------------------------------------------------------------------
 constexpr int FWD_THREADS = 256;
 constexpr int FWD_PR = 4;                          // pool rows per block
@@ -174,14 +222,20 @@ constexpr int FWD_PARTS = PL / FWD_PR;             // blocks per image
 constexpr int FWD_C1R = 2 * FWD_PR + 2;            // conv1 rows per block
 constexpr int FWD_IMR = FWD_C1R + 2;               // image rows per block
 constexpr int FWD_C1T = (FWD_C1R * A1 + 31) / 32;  // conv1 tiles (9)
-static_assert(FWD_PR * PL / 8 == 6, "6 row tiles per block: 2 wave groups x 3");
+constexpr int FWD_TILES = FWD_PR * PL;             // 48 Winograd tiles (= pool windows) per block
+constexpr int FWD_TQ = 16 * C2 + 16;               // one (row i, b) plane of T for a 16-tile group (+pad)
 
-__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_fwd_kernel(
+__device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
-    int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, float* __restrict__ pooled,
-    uint8_t* __restrict__ code) {
+    int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, const float* __restrict__ U,
+    float* __restrict__ pooled, uint8_t* __restrict__ code) {
   __shared__ float img_s[FWD_IMR * IMG];
   __shared__ float a1_s[FWD_C1R * A1 * A1P];
+  __shared__ float t_s[8 * FWD_TQ];  // [i][b][16 tiles][64 co]
   const int64_t lb = xcd_block();  // logical block (part, j, r), replica-major
   const int part = (int)(lb % FWD_PARTS);
   const int j = (int)((lb / FWD_PARTS) % gridDim.y);
@@ -208,7 +262,6 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   const int wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
-  const int nt = wave & 1, tg = wave >> 1;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
   __syncthreads();
@@ -229,65 +282,101 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   }
   __syncthreads();
 
-  int pbase[3];
+  // ---- Winograd GEMMs: wave = transform row i; lane (tl = lane & 15, kq = lane >> 4)
+  const int wi = wave;
+  const int tl = lane & 15, kq = lane >> 4;
+  // B^T row i combines input rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  int pa[3];  // this lane's patch origin (row 2ty + ra, col 2tx) in a1_s for each tile group, + channel kq
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int t = 3 * tg + u;
-    const int wi = 8 * t + (m >> 2);
-    const int pr = wi / PL, pc = wi % PL;
-    const int q = m & 3;
-    const int oy = 2 * pr + (q >> 1), ox = 2 * pc + (q & 1);
-    pbase[u] = (oy * A1 + ox) * A1P;
+  for (int g = 0; g < 3; ++g) {
+    const int tile = 16 * g + tl;
+    const int ty = tile / PL, tx = tile % PL;
+    pa[g] = ((2 * ty + ra) * A1 + 2 * tx) * A1P + kq;
   }
-  floatx16 acc[3];
+  const int drow = (rb - ra) * A1 * A1P;
+  const float* Ub = U + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C1 * C2 + kq * C2 + tl;
+  auto load_b = [&](int st, float (&bv)[16]) {
 #pragma unroll
-  for (int u = 0; u < 3; ++u) acc[u] = zero16();
-  // K = 9 taps x 32 channels in 18 groups of 8 channel pairs; the B operand (this wave's 32 columns of W2,
-  // L2-resident) of group g + 1 is loaded into registers while group g's MFMAs run
-  const float* W2 = P + OFF_W2 + kh * C2 + nt * 32 + m;
-  float bcur[8], bnxt[8];
-  auto load_b = [&](int g, float (&b)[8]) {
-    const float* w = W2 + (int64_t)((g >> 1) * C1 + (g & 1) * 16) * C2;
+    for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = w[2 * i * C2];
+      for (int cg = 0; cg < 4; ++cg) bv[4 * jj + cg] = Ub[(int64_t)jj * C1 * C2 + (4 * st) * C2 + 16 * cg];
   };
-  load_b(0, bcur);
-#pragma unroll
-  for (int g = 0; g < 18; ++g) {
-    if (g + 1 < 18) load_b(g + 1, bnxt);
-    const int kyx = g >> 1, ky = kyx / 3, kx = kyx % 3;
-    const int off = (ky * A1 + kx) * A1P + (g & 1) * 16 + kh;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int u = 0; u < 3; ++u) acc[u] = mfma32(a1_s[pbase[u] + off + 2 * i], bcur[i], acc[u]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) bcur[i] = bnxt[i];
-  }
-  // epilogue: bias, ReLU, 2x2 max-pool (first max in window scan order), argmax code
   float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
   uint8_t* outc = code ? code + ((int64_t)r * bmax + j) * FEAT : nullptr;
-  const int co = nt * 32 + m;
-  const float bias = P[OFF_B2 + co];
+#pragma unroll 1
+  for (int g = 0; g < 3; ++g) {  // one 16-tile group at a time
+    fvec4 acc[4][4];             // [j][channel group]
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int t = 3 * tg + u;
+    for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int wi = 8 * t + 2 * g + kh;
-      const int py = FWD_PR * part + wi / PL, px = wi % PL;
-      float best = acc[u][4 * g] + bias;
+      for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    float bcur[16], bnxt[16];
+    load_b(0, bcur);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      if (st + 1 < 8) load_b(st + 1, bnxt);
+      const float* d0 = a1_s + pa[g] + 4 * st;
+      float t[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * A1P] + sb * d0[drow + c * A1P];
+      float v[4];
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = mfma16(v[jj], bcur[4 * jj + cg], acc[jj][cg]);
+      if (st + 1 < 8) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) bcur[q] = bnxt[q];
+      }
+    }
+    // T_i[b] = sum_j M_ij A[j][b]: T_i0 = M_i0 + M_i1 + M_i2, T_i1 = M_i1 - M_i2 - M_i3.  Lane holds tiles
+    // 4*kq + rr (rr = 0..3) of the group, channel 16*cg + tl.
+#pragma unroll
+    for (int cg = 0; cg < 4; ++cg)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float m0 = acc[0][cg][rr], m1 = acc[1][cg][rr], m2 = acc[2][cg][rr], m3 = acc[3][cg][rr];
+        const int o = (4 * kq + rr) * C2 + 16 * cg + tl;
+        t_s[(2 * wi) * FWD_TQ + o] = (m0 + m1) + m2;
+        t_s[(2 * wi + 1) * FWD_TQ + o] = (m1 - m2) - m3;
+      }
+    __syncthreads();
+    // Y[a][b] = sum_i A^T[a][i] T_i[b]: Y0b = T0b + T1b + T2b, Y1b = T1b - T2b - T3b; window pixel q = 2a + b
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = tid + FWD_THREADS * k;  // (tile in group, co)
+      const int co = o & 63;
+      const int tile = 16 * g + (o >> 6);
+      float tv[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * FWD_TQ + o];
+      const float bias = P[OFF_B2 + co];
+      float z[4];
+      z[0] = ((tv[0][0] + tv[1][0]) + tv[2][0]) + bias;
+      z[1] = ((tv[0][1] + tv[1][1]) + tv[2][1]) + bias;
+      z[2] = ((tv[1][0] - tv[2][0]) - tv[3][0]) + bias;
+      z[3] = ((tv[1][1] - tv[2][1]) - tv[3][1]) + bias;
+      float best = z[0];
       int arg = 0;
 #pragma unroll
-      for (int qq = 1; qq < 4; ++qq) {
-        const float z = acc[u][4 * g + qq] + bias;
-        if (z > best) { best = z; arg = qq; }
-      }
+      for (int qq = 1; qq < 4; ++qq)
+        if (z[qq] > best) { best = z[qq]; arg = qq; }
+      const int py = FWD_PR * part + tile / PL, px = tile % PL;
       const int pidx = (py * PL + px) * C2 + co;
       outp[pidx] = fmaxf(best, 0.0f);
       if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
     }
+    __syncthreads();
   }
 }
 
@@ -811,10 +900,6 @@ constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // pooled pairs per thread per
 constexpr int WG_A1H = 6 * A1 * 16 + 16;  // one ci-half plane of the band's conv1 rows (+16: write banks)
 constexpr int WG_DZQ = 4 * Z2 * 16 + 16;  // one co-quarter plane of the band's dense dZ2 (+16: write banks)
 
-__device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
 // K loop over one band's 96 conv2 pixels, four per MFMA (px = 4*s4 + (lane >> 4)), for row half RH
 // (compile-time, so every LDS offset is an immediate).
 template <int RH>
@@ -1082,9 +1167,11 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t);
+  // t->w2t holds W2 in Winograd form for the forward, then (transpose_w2) W2 transposed for the data gradient
+  winograd_w2_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(1);
-  conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->pooled,
-                                                         t->code);
+  conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->w2t,
+                                                         t->pooled, t->code);
   PROF_END(1);
   PROF_BEGIN(2);
   dense_fwd_kernel<<<dim3((B + 31) / 32, R), 256, 0, s>>>(t->pooled, (int64_t)B * FEAT, t->cnt, 0, B, t->params, S,
@@ -1117,16 +1204,17 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
 }
 
 int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
-                      int n_samples, int chunk, float* pooled, float* hidden, int32_t* correct, double* loss_sum,
-                      void* stream) {
-  if (!params || !x || !labels || !pooled || !hidden || !correct || !loss_sum) return MPLC_E_ARG;
+                      int n_samples, int chunk, float* pooled, float* hidden, float* w2_wino, int32_t* correct,
+                      double* loss_sum, void* stream) {
+  if (!params || !x || !labels || !pooled || !hidden || !w2_wino || !correct || !loss_sum) return MPLC_E_ARG;
   if (n_models < 1 || n_models > 65535 || n_samples < 1 || chunk < 1 || chunk > 65535 || stride != MPLC_CNN_STRIDE)
     return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
+  winograd_w2_kernel<<<dim3(C1 * C2 / 256, n_models), 256, 0, s>>>(params, stride, nullptr, w2_wino);
   for (int s0 = 0; s0 < n_samples; s0 += chunk) {
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
     conv_fwd_kernel<<<dim3(FWD_PARTS, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
-                                                                  pooled, nullptr);
+                                                                  w2_wino, pooled, nullptr);
     dense_fwd_kernel<<<dim3((cn + 31) / 32, n_models), 256, 0, s>>>(pooled, (int64_t)chunk * FEAT, nullptr, cn, chunk,
                                                                     params, stride, hidden);
     eval_head_kernel<<<n_models, 256, 0, s>>>(hidden, cn, chunk, labels, s0, params, stride, correct, loss_sum);

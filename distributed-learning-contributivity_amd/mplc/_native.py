@@ -37,7 +37,7 @@ SIGNATURES = {
     "mplc_seq_snapshot": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                   c_int, c_void_p, c_void_p, c_void_p]),
     "mplc_cnn_evaluate": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                  c_void_p, c_void_p, c_void_p]),
+                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     # batched CIFAR10 CNN trainer (include/mplc_hip_cifar.h); mplc.cifar re-binds train_step with its struct
     "mplc_cifar_stride": (c_int, []),
     "mplc_cifar_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),

