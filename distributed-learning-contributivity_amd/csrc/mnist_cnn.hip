@@ -1,16 +1,18 @@
 // Batched multi-model MNIST CNN trainer for gfx950 (see include/mplc_hip_cnn.h for the contract).
 //
-// One lockstep step of B replicas = 9 launches:
+// One lockstep step of B replicas = 10 launches:
 //   schedule        per replica: this step's sample rows, batch count, Adam step     (index work)
-//   conv_fwd        conv1 (recomputed, VALU) -> conv2 implicit GEMM on fp32 MFMA 32x32x2 -> +b, ReLU,
-//                   2x2 max-pool fused in the accumulator layout -> pooled + argmax code
+//   winograd_w2     W2 in Winograd form (G g G^T per input/output channel pair)
+//   conv_fwd        conv1 (recomputed, MFMA) -> conv2 in Winograd form F(2x2,3x3) on fp32 MFMA 16x16x4 (one
+//                   output tile = one pooling window) -> +b, ReLU, 2x2 max-pool -> pooled + argmax code
 //   dense_fwd       Dense(128)+ReLU: per-replica GEMM [b x 9216] x [9216 x 128], fp32 MFMA
 //   head            Dense(10), softmax-CE gradient, dW4/db4 + Adam, dh = dlogits W4^T * relu'
 //   dense1_bwd_adam per 64-row slice of W3: dp = dh W3^T, dW3 = p^T dh, Adam(W3) in the same pass
 //                   (W3 = 98% of the parameters: read once, written once per step)
-//   transpose_w2    W2 [kyx][ci][co] -> [kyx][co][ci] for coalesced MFMA B-fragments in the dgrad
-//   conv_bwd_data   dA1 = dZ2 (*) W2 on MFMA, dZ2 rebuilt on the fly from (dp, argmax code); ReLU' of
-//                   the recomputed conv1 output and conv1's weight gradient fused in the epilogue
+//   winograd_w2r    W2 rotated by 180 degrees, channels swapped, in Winograd form (dgrad B operand)
+//   conv_bwd_data   dA1 = dZ2 (*) W2 in Winograd form F(2x2,3x3) on MFMA, V built directly from (dp, argmax
+//                   code) of the 2x2 pooling windows a tile's patch covers; ReLU' of the recomputed conv1
+//                   output and conv1's weight gradient fused in the epilogue
 //   conv_wgrad      dW2 = A1^T dZ2 on MFMA over all pixels of a replica's samples (split-K partials)
 //   adam_small      Adam on W1/b1/W2/b2 from the per-sample / per-split partials (fixed order: bitwise
 //                   reproducible)
@@ -223,7 +225,8 @@ constexpr int FWD_C1R = 2 * FWD_PR + 2;            // conv1 rows per block
 constexpr int FWD_IMR = FWD_C1R + 2;               // image rows per block
 constexpr int FWD_C1T = (FWD_C1R * A1 + 31) / 32;  // conv1 tiles (9)
 constexpr int FWD_TILES = FWD_PR * PL;             // 48 Winograd tiles (= pool windows) per block
-constexpr int FWD_TQ = 16 * C2 + 16;               // one (row i, b) plane of T for a 16-tile group (+pad)
+constexpr int FWD_TS = C2 + 1;                     // tile stride of a T plane (odd: conflict-free writes)
+constexpr int FWD_TQ = 16 * FWD_TS;                // one (row i, b) plane of T for a 16-tile group
 
 __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const float m0 = acc[0][cg][rr], m1 = acc[1][cg][rr], m2 = acc[2][cg][rr], m3 = acc[3][cg][rr];
-        const int o = (4 * kq + rr) * C2 + 16 * cg + tl;
+        const int o = (4 * kq + rr) * FWD_TS + 16 * cg + tl;
         t_s[(2 * wi) * FWD_TQ + o] = (m0 + m1) + m2;
         t_s[(2 * wi + 1) * FWD_TQ + o] = (m1 - m2) - m3;
       }
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * FWD_TQ + o];
+        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * FWD_TQ + (o >> 6) * FWD_TS + co];
       const float bias = P[OFF_B2 + co];
       float z[4];
       z[0] = ((tv[0][0] + tv[1][0]) + tv[2][0]) + bias;
@@ -705,177 +708,268 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   }
 }
 
-// W2 [kyx][ci][co] -> W2t [kyx][co][ci]
-__global__ void transpose_w2_kernel(const float* __restrict__ params, int64_t stride, const int32_t* __restrict__ cnt,
-                                    float* __restrict__ w2t) {
+// W2 for the data gradient in Winograd form: the data gradient is the correlation of the padded dZ2 with
+// the kernel rotated by 180 degrees and its channels swapped, W2r[ky][kx][co][ci] = W2[2-ky][2-kx][ci][co];
+// Ur[xi = 4i + j][co][ci] = (G W2r G^T)[i][j]  (ci contiguous: the B operand of the dgrad GEMMs).
+__global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restrict__ params, int64_t stride,
+                                                           const int32_t* __restrict__ cnt, float* __restrict__ Ur) {
   const int r = blockIdx.y;
   if (cnt && cnt[r] == 0) return;
-  const float* W2 = params + (int64_t)r * stride + OFF_W2;
-  float* T = w2t + (int64_t)r * (9 * C1 * C2);
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 9 * C1 * C2; e += gridDim.x * blockDim.x) {
-    const int kyx = e / (C1 * C2);
-    const int rem = e % (C1 * C2);
-    const int co = rem / C1, ci = rem % C1;
-    T[e] = W2[(kyx * C1 + ci) * C2 + co];
+  const int e = blockIdx.x * 256 + threadIdx.x;  // (co, ci) of the output
+  if (e >= C1 * C2) return;
+  const int co = e / C1, ci = e % C1;
+  const float* W2 = params + (int64_t)r * stride + OFF_W2 + ci * C2 + co;  // tap k at W2[k * C1 * C2]
+  float g[3][3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) g[ky][kx] = W2[((2 - ky) * 3 + (2 - kx)) * C1 * C2];
+  float gg[4][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const float col[3] = {g[0][kx], g[1][kx], g[2][kx]};
+    float o[4];
+    wino_g_rows(col, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
+  }
+  float* U = Ur + (int64_t)r * MPLC_CNN_W2T + e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float o[4];
+    wino_g_rows(gg[i], o);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) U[(4 * i + jj) * C1 * C2] = o[jj];
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv2 data gradient + conv1 backward.  Block = (sample, band of 13 conv1 rows), 4 waves.
-// dA1[pos][ci] = sum_{ky,kx,co} dZ2[pos-(ky,kx)][co] W2[ky][kx][ci][co]  (implicit GEMM, K = 9 x 64)
-// dZ2 (the max-pool gradient, 3/4 zeros) is un-pooled from (dp, argmax code) into a dense LDS tile
-// [15 rows][28 cols (2 zero columns each side)][17] one quarter of the channels (16) at a time; every
-// A-operand read is then one ds_read_b32 at a compile-time offset from a per-lane base.  B (W2
-// transposed, [kyx][co][ci]) streams from L2.  The next quarter's (dp, code) are fetched into registers
-// while the current quarter's MFMAs run.  Epilogue on MFMA too: conv1 recomputed (conv1_mfma), ReLU'
-// applied, and dW1/db1 = patch^T dZ1 as 16 MFMAs per tile with the masked accumulators as B operand.
+// conv2 data gradient + conv1 backward, Winograd F(2x2, 3x3).  Block = (band of 48 output tiles, sample,
+// replica), 4 waves.  dA1[y][x][ci] = sum_{ky,kx,co} dZ2p[y+ky][x+kx][co] W2r[ky][kx][co][ci] (dZ2p = dZ2
+// padded by 2): 13 x 13 output tiles of 2x2 in row-major order, 16 GEMMs M[xi][tile][ci] = sum_co
+// V[xi][tile][co] Ur[xi][co][ci], K = 64 output channels of conv2.
+// The band's rows of dZ2 (the max-pool gradient: one nonzero per window, at its argmax when positive) are
+// un-pooled from (dp, code) into a dense LDS tile one quarter of the channels (16) at a time, with zero
+// rows / columns around the 12 x 12 grid, so a tile's 4x4 patch is read without tests.  Wave i owns
+// transform row i (xi = 4i .. 4i+3) of the band's three 16-tile groups x both 16-channel halves of ci
+// (24 accumulators of v_mfma_f32_16x16x4_f32): per k-step a lane reads 2 patch rows (8 values), forms its
+// 4 values of V with 8 adds, and issues 24 MFMAs with 8 B operands (Ur, L2-resident) loaded one k-step
+// ahead.  Epilogue per group: each wave folds its row of the output transform into LDS; then every wave takes
+// 4 tiles (16 positions): dA1 = sum_i A^T T_i, dZ1 = dA1 * ReLU'(conv1) (conv1 recomputed on MFMA by
+// conv1_mfma, bit-identical to the forward's), and [dW1 | db1] += patch^T dZ1 on MFMA (rows = 9 taps + bias);
+// one partial per (sample, band), the waves' partials added in a fixed order.
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_THREADS = 256;
-constexpr int BAND = 13;               // conv1 rows per block (2 bands cover 26 rows)
-constexpr int BAND_POS = BAND * A1;    // 338 positions
-constexpr int BAND_TILES = 11;         // ceil(338 / 32)
-constexpr int DZR = BAND + 2;          // dZ2 rows a band needs
-constexpr int DZC = Z2 + 4;            // dZ2 columns incl. 2 zero columns each side
-constexpr int DZQ = 17;                // padded channel stride (16 channels per quarter)
-constexpr int BWD_PRE = 6;             // pooled (dp, code) pairs per thread per quarter: 8 rows x 12 x 16 / 256
+constexpr int BWD_TILES = 169;                 // 13 x 13 output tiles of 2 x 2 over the 26 x 26 conv1 grid
+constexpr int BWD_BAND_TILES = 48;             // tiles per block (3 groups of 16)
+constexpr int BWD_BANDS = 4;                   // ceil(169 / 48)
+constexpr int BWD_WR = 6;                      // window rows a band's patches touch (tile rows + 1)
+constexpr int BWD_DR = 2 * BWD_WR;             // dZ2 rows staged
+constexpr int BWD_DC = Z2 + 4;                 // dZ2 columns staged: 2 zero columns each side
+constexpr int BWD_CS = 17;                     // channel stride (16 channels of a quarter + 1: bank spread)
+constexpr int BWD_TS = C1 + 1;                 // tile stride of a T plane (odd: conflict-free writes)
+constexpr int BWD_TQ = 16 * BWD_TS;            // one (row i, b) plane of T for a 16-tile group
+constexpr int BWD_PRE = (BWD_WR * PL * 16 + BWD_THREADS - 1) / BWD_THREADS;  // (dp, code) pairs per thread
 
-// One channel quarter of the dgrad GEMM for NT tiles (branch-free; NT is 3 for waves 0-2, 2 for wave 3).
-template <int NT>
-__device__ __forceinline__ void bwd_data_quarter(const float* dz_s, const int (&abase)[3], const float* Tq,
-                                                 floatx16 (&acc)[3]) {
-#pragma unroll
-  for (int kyx = 0; kyx < 9; ++kyx) {
-    const int ky = kyx / 3, kx = kyx % 3;
-    const int offA = ((2 - ky) * DZC + (2 - kx)) * DZQ;
-    const float* Tk = Tq + kyx * C2 * C1;
-    float b[8];
-#pragma unroll
-    for (int c2 = 0; c2 < 8; ++c2) b[c2] = Tk[2 * c2 * C1];
-#pragma unroll
-    for (int c2 = 0; c2 < 8; ++c2) {
-#pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mfma32(dz_s[abase[u] + offA + 2 * c2], b[c2], acc[u]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_bwd_data_kernel(
+__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_bwd_data_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
-    const float* __restrict__ params, int64_t stride, const float* __restrict__ w2t,
+    const float* __restrict__ params, int64_t stride, const float* __restrict__ Ur,
     const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
-  __shared__ float dz_s[DZR * DZC * DZQ];
-  __shared__ float img_s[(BAND + 2) * IMG];
+  __shared__ float dz_s[BWD_DR * BWD_DC * BWD_CS];
+  __shared__ float img_s[IMG * IMG];
+  __shared__ float t_s[8 * BWD_TQ];
   __shared__ float red_s[4][10 * 32];
   const int64_t lb = xcd_block();  // logical block (band, j, r), replica-major
-  const int band = (int)(lb & 1);
-  const int j = (int)((lb % gridDim.x) >> 1);
-  const int r = (int)(lb / gridDim.x);
+  const int band = (int)(lb % BWD_BANDS);
+  const int j = (int)((lb / BWD_BANDS) % gridDim.y);
+  const int r = (int)(lb / ((int64_t)BWD_BANDS * gridDim.y));
   if (j >= cnt[r]) return;
   const int tid = threadIdx.x;
   const int row = idx[(int64_t)r * bmax + j];
   const float* P = params + (int64_t)r * stride;
+  const int tile0 = band * BWD_BAND_TILES;
+  const int ngroups = min(3, (BWD_TILES - tile0 + 15) / 16);
+  const int ty0 = tile0 / 13;
+  const int wy0 = ty0 - 1;  // first window row staged (local window row 0; rows outside 0..11 stay zero)
   const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
   const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
-  const int iy0 = band * BAND;
-  const int oy0 = iy0 - 2;             // dZ2 row of local row 0
-  const int pr0 = (oy0 + 2) / 2 - 1;  // first pooled row touching the band (-1 or 5)
-  for (int e = tid; e < DZR * DZC * DZQ; e += BWD_THREADS) dz_s[e] = 0.0f;
-  {
-    constexpr int NIT = ((BAND + 2) * IMG + BWD_THREADS - 1) / BWD_THREADS;
-    const float* xr = x + (int64_t)row * IMG * IMG + iy0 * IMG;
-    float v[NIT];
-#pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int e = tid + BWD_THREADS * k;
-      v[k] = xr[e < (BAND + 2) * IMG ? e : 0];
-    }
-#pragma unroll
-    for (int k = 0; k < NIT; ++k)
-      if (tid + BWD_THREADS * k < (BAND + 2) * IMG) img_s[tid + BWD_THREADS * k] = v[k];
-  }
-  const int lane = tid & 63, wave = tid >> 6;
-  const int n = lane & 31;
-  const int kh = lane >> 5;
-  // pooled pair e = tid + 256*s of a quarter: channel e&15, pooled col (e>>4)%12, pooled row pr0 + e/192
+  // pair e of a quarter: channel e & 15, window column (e >> 4) % 12, local window row e / 192
   float pdv[BWD_PRE];
   uint32_t pcd[BWD_PRE];
   auto fetch = [&](int q) {
 #pragma unroll
     for (int s = 0; s < BWD_PRE; ++s) {
       const int e = tid + BWD_THREADS * s;
-      const int py = pr0 + e / 192;
-      const int pidx = (py * PL + (e >> 4) % PL) * C2 + q * 16 + (e & 15);
-      const bool ok = py >= 0 && py < PL;
+      const int wy = wy0 + e / (PL * 16);
+      const bool ok = e < BWD_WR * PL * 16 && wy >= 0 && wy < PL;
+      const int pidx = (wy * PL + (e >> 4) % PL) * C2 + 16 * q + (e & 15);
       pdv[s] = ok ? dp[pidx] : 0.0f;
       pcd[s] = ok ? cd[pidx] : 0u;
     }
   };
   fetch(0);
-  const float* T = w2t + (int64_t)r * (9 * C1 * C2) + kh * C1 + n;
-  const int ntile = (wave + 8 < BAND_TILES) ? 3 : 2;
-  floatx16 acc[3];
-  int abase[3];
+  {
+    constexpr int NIT = (IMG * IMG + BWD_THREADS - 1) / BWD_THREADS;
+    const float* xr = x + (int64_t)row * IMG * IMG;
+    float v[NIT];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    acc[u] = zero16();
-    const int pl = min((wave + 4 * u) * 32 + n, BAND_POS - 1);
-    abase[u] = ((pl / A1) * DZC + pl % A1) * DZQ + kh;
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + BWD_THREADS * k;
+      v[k] = xr[e < IMG * IMG ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k)
+      if (tid + BWD_THREADS * k < IMG * IMG) img_s[tid + BWD_THREADS * k] = v[k];
+    // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
+    for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
+      const int rr = e / (4 * BWD_CS), c = (e / BWD_CS) % 4, k = e % BWD_CS;
+      dz_s[(rr * BWD_DC + (c < 2 ? c : BWD_DC - 4 + c)) * BWD_CS + k] = 0.0f;
+    }
   }
-  for (int q = 0; q < 4; ++q) {
-    __syncthreads();  // zero fill done / previous quarter's readers done
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31;
+  const int kh = lane >> 5;
+  float w1r[5];
+  load_w1r(P, kh, n, w1r);
+  // GEMM roles: wave = transform row i; lane (tl = lane & 15: tile in group / ci in half, kq = lane >> 4)
+  const int wi = wave;
+  const int tl = lane & 15, kq = lane >> 4;
+  // B^T row i combines patch rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  int pa[3];  // this lane's patch origin (staged row 2*(ty - ty0) + ra, column 2*tx) per group, + channel kq
 #pragma unroll
-    for (int s = 0; s < BWD_PRE; ++s) {
+  for (int g = 0; g < 3; ++g) {
+    const int t = min(tile0 + 16 * g + tl, BWD_TILES - 1);
+    const int ty = t / 13, tx = t % 13;
+    pa[g] = ((2 * (ty - ty0) + ra) * BWD_DC + 2 * tx) * BWD_CS + kq;
+  }
+  const int drow = (rb - ra) * BWD_DC * BWD_CS;
+  const float* Ub = Ur + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C2 * C1 + kq * C1 + tl;
+  auto load_b = [&](int k4, float (&bv)[8]) {  // k4: global k-step (channels 4*k4 .. 4*k4+3)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) bv[2 * jj + ch] = Ub[(int64_t)jj * C2 * C1 + (4 * k4) * C1 + 16 * ch];
+  };
+  fvec4 acc[3][4][2];  // [group][j][ci half]
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) acc[g][jj][ch] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  float bcur[8], bnxt[8];
+  load_b(0, bcur);
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {  // channel quarters
+    __syncthreads();             // previous quarter's readers done (and the zero columns / image written)
+#pragma unroll
+    for (int s = 0; s < BWD_PRE; ++s) {  // un-pool the quarter's (dp, code) into the dense band
       const int e = tid + BWD_THREADS * s;
-      const int py = pr0 + e / 192;
-      const int pc = (e >> 4) % PL;
-      const int ch = e & 15;
-      const uint32_t c = pcd[s];
-      const float v = (c & 0x80) ? pdv[s] : 0.0f;
-      const int sel = c & 3;
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy) {
-        const int lr = 2 * py + dy - oy0;
-        if (py >= 0 && py < PL && lr >= 0 && lr < DZR) {
-          float* d = dz_s + (lr * DZC + 2 * pc + 2) * DZQ + ch;
-          d[0] = (sel == 2 * dy) ? v : 0.0f;
-          d[DZQ] = (sel == 2 * dy + 1) ? v : 0.0f;
-        }
+      if (e < BWD_WR * PL * 16) {
+        const int lwy = e / (PL * 16), wx = (e >> 4) % PL, ch = e & 15;
+        const uint32_t c = pcd[s];
+        const float v = (c & 0x80) ? pdv[s] : 0.0f;
+        const int sel = c & 3;
+        float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
+        d[0] = (sel == 0) ? v : 0.0f;
+        d[BWD_CS] = (sel == 1) ? v : 0.0f;
+        d[BWD_DC * BWD_CS] = (sel == 2) ? v : 0.0f;
+        d[BWD_DC * BWD_CS + BWD_CS] = (sel == 3) ? v : 0.0f;
       }
     }
     if (q < 3) fetch(q + 1);
     __syncthreads();
-    if (ntile == 3) bwd_data_quarter<3>(dz_s, abase, T + q * 16 * C1, acc);
-    else bwd_data_quarter<2>(dz_s, abase, T + q * 16 * C1, acc);
-  }
-  // epilogue: dZ1 = dA1 * ReLU'(conv1), then [dW1 | db1] += patch^T dZ1 on MFMA (rows = 9 taps + bias)
-  float w1r[5];
-  load_w1r(P, kh, n, w1r);
-  const int toff = (n < 9) ? (n / 3) * IMG + n % 3 : 0;
-  floatx16 g = zero16();
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    if (u >= ntile) break;
-    const int t = wave + 4 * u;
-    const int pl = min(t * 32 + n, BAND_POS - 1);
-    const floatx16 a1 = conv1_mfma(img_s, (pl / A1) * IMG + pl % A1, kh, w1r);
+    for (int st = 0; st < 4; ++st) {
+      const int k4 = 4 * q + st;
+      if (k4 + 1 < 16) load_b(k4 + 1, bnxt);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int pr = t * 32 + acc_row(reg, kh);
-      const float dz = (a1[reg] > 0.0f) ? acc[u][reg] : 0.0f;
-      const int prc = min(pr, BAND_POS - 1);
-      const float pv = img_s[(prc / A1) * IMG + prc % A1 + toff];
-      const float av = (pr < BAND_POS && n < 10) ? (n < 9 ? pv : 1.0f) : 0.0f;
-      g = mfma32(av, dz, g);
+      for (int g = 0; g < 3; ++g) {
+        const float* d0 = dz_s + pa[g] + 4 * st;
+        float t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * BWD_CS] + sb * d0[drow + c * BWD_CS];
+        float v4[4];
+        v4[0] = t[0] - t[2];
+        v4[1] = t[1] + t[2];
+        v4[2] = t[2] - t[1];
+        v4[3] = t[1] - t[3];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch) acc[g][jj][ch] = mfma16(v4[jj], bcur[2 * jj + ch], acc[g][jj][ch]);
+      }
+      if (k4 + 1 < 16) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bcur[k] = bnxt[k];
+      }
     }
   }
-  // g: rows = tap (0..9), cols = ci; rows 0..9 live in regs 0..3 (kh 0: rows 0-3, kh 1: rows 4-7), 4..5 (kh 0)
+  const int toff = (n < 9) ? (n / 3) * IMG + n % 3 : 0;  // dW1 A operand: tap n of a position
+  floatx16 gacc = zero16();                              // [dW1 | db1] partial: rows = tap, cols = ci
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    if (g >= ngroups) break;
+    __syncthreads();  // previous group's T readers done
+    // T_i[b] = sum_j M_ij A[j][b] into LDS: lane holds tiles 4*kq + rr of the group, ci 16*ch + tl
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float m0 = acc[g][0][ch][rr], m1 = acc[g][1][ch][rr], m2 = acc[g][2][ch][rr], m3 = acc[g][3][ch][rr];
+        const int o = (4 * kq + rr) * BWD_TS + 16 * ch + tl;
+        t_s[(2 * wi) * BWD_TQ + o] = (m0 + m1) + m2;
+        t_s[(2 * wi + 1) * BWD_TQ + o] = (m1 - m2) - m3;
+      }
+    __syncthreads();
+    // wave w takes tiles 4w .. 4w+3 of the group = 16 positions m = 4*(tile) + q (q = 2dy+dx); conv1_mfma
+    // rows m (lanes 0-15 of each half; rows 16-31 repeat them and are not used)
+    const int m = n & 15;
+    const int tq = tile0 + 16 * g + 4 * wave + (m >> 2);
+    const int tqc = min(tq, BWD_TILES - 1);
+    const int py = 2 * (tqc / 13) + ((m & 3) >> 1), px = 2 * (tqc % 13) + (m & 1);
+    const floatx16 a1 = conv1_mfma(img_s, py * IMG + px, kh, w1r);
+    // lane (n = ci, kh) holds positions acc_row(reg, kh): reg 0..3 -> tile kh, q = reg; reg 4..7 -> tile 2+kh
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tg = 4 * wave + 2 * h + kh;  // tile within the group
+      const int tt = tile0 + 16 * g + tg;
+      float tv[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * BWD_TQ + tg * BWD_TS + n];
+      float y[4];
+      y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
+      y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
+      y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
+      y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
+      const int ttc = min(tt, BWD_TILES - 1);
+      const bool valid = tt < BWD_TILES && tt < tile0 + BWD_BAND_TILES;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int reg = 4 * h + qq;
+        const float dz = (valid && a1[reg] > 0.0f) ? y[qq] : 0.0f;
+        // A operand: tap n (< 9) of this lane-half's position, 1 for the bias row
+        const int qy = 2 * (ttc / 13) + (qq >> 1), qx = 2 * (ttc % 13) + (qq & 1);
+        const float pv = img_s[qy * IMG + qx + toff];
+        const float av = (n < 10) ? (n < 9 ? pv : 1.0f) : 0.0f;
+        gacc = mfma32(av, dz, gacc);
+      }
+    }
+  }
+  // gacc: rows = tap (0..9), cols = ci; rows 0..9 live in regs 0..3 (kh 0: rows 0-3, kh 1: rows 4-7), 4..5 (kh 0)
 #pragma unroll
   for (int reg = 0; reg < 8; ++reg) {
     const int k = acc_row(reg, kh);
-    if (k < 10) red_s[wave][k * 32 + n] = g[reg];
+    if (k < 10) red_s[wave][k * 32 + n] = gacc[reg];
   }
   __syncthreads();
-  float* out = w1_part + (((int64_t)r * bmax + j) * 2 + band) * MPLC_CNN_W1P;
+  float* out = w1_part + (((int64_t)r * bmax + j) * BWD_BANDS + band) * MPLC_CNN_W1P;
   for (int e = tid; e < 10 * 32; e += BWD_THREADS)
     out[e] = (red_s[0][e] + red_s[1][e]) + (red_s[2][e] + red_s[3][e]);
 }
@@ -1060,8 +1154,8 @@ __global__ void adam_small_kernel(const int32_t* __restrict__ cnt, const int32_t
   if (e >= OFF_W3) return;
   float g = 0.0f;
   if (e < OFF_W2) {
-    const float* w = w1_part + (int64_t)r * bmax * 2 * MPLC_CNN_W1P + e;
-    for (int jj = 0; jj < 2 * count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];  // (sample, band) order
+    const float* w = w1_part + (int64_t)r * bmax * BWD_BANDS * MPLC_CNN_W1P + e;
+    for (int jj = 0; jj < BWD_BANDS * count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];  // (sample, band) order
   } else {
     const float* w = w2_part + (int64_t)r * splits * MPLC_CNN_W2P + (e - OFF_W2);
     const int used = (count + WG_SAMPLES - 1) / WG_SAMPLES;
@@ -1167,7 +1261,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t);
-  // t->w2t holds W2 in Winograd form for the forward, then (transpose_w2) W2 transposed for the data gradient
+  // t->w2t holds W2 in Winograd form for the forward, then the rotated kernel's Winograd form for the dgrad
   winograd_w2_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(1);
   conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->w2t,
@@ -1186,9 +1280,9 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                                   t->params, t->adam_m, t->adam_v, S, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
   PROF_END(4);
-  transpose_w2_kernel<<<dim3(18, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
+  winograd_w2r_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(5);
-  conv_bwd_data_kernel<<<dim3(2 * B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
+  conv_bwd_data_kernel<<<dim3(BWD_BANDS, B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
                                                           t->code, t->w1_part);
   PROF_END(5);
   PROF_BEGIN(6);

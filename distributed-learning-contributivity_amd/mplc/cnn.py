@@ -26,6 +26,7 @@ FEAT = 9216
 HID = 128
 W1P = 320
 W2P = 18496
+W1_BANDS = 4  # MPLC_CNN_W1_BANDS: [dW1 | db1] partials per sample (data-gradient blocks)
 W2T = 32768  # MPLC_CNN_W2T: W2 in Winograd form (forward), then transposed (data gradient)
 WG_SAMPLES = 8
 PATIENCE = 10
@@ -180,7 +181,7 @@ class MnistModel:
         self.lib = _native.lib()
 
     def replica_bytes(self, bmax):
-        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + 2 * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
+        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + W1_BANDS * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
                 + W2T * 4 + bmax * 12)
 
     def init_params(self, glob, keys, stream):
@@ -200,7 +201,7 @@ class MnistModel:
             idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
             pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
             hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
-            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, 2, W1P), **f32),
+            dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, W1_BANDS, W1P), **f32),
             w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, W2T), **f32))
         t = TrainT()
         t.n_rep, t.bmax, t.w2_splits = R, B, splits

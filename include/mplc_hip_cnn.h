@@ -43,6 +43,7 @@ extern "C" {
 #define MPLC_CNN_OFF_B4 1199872    /* 10         */
 #define MPLC_CNN_NPARAM 1199882
 #define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
+#define MPLC_CNN_W1_BANDS 4        /* data-gradient blocks per sample (48 Winograd tiles each) */
 #define MPLC_CNN_W2T 32768         /* per-model W2 workspace: 16 Winograd planes x 32 x 64 floats */
 #define MPLC_CNN_FEAT 9216         /* flattened pooled features */
 #define MPLC_CNN_HID 128
@@ -103,10 +104,11 @@ typedef struct {
   float* hidden;          /* [n_rep][bmax][128]                                           */
   float* dhidden;         /* [n_rep][bmax][128]                                           */
   float* dpooled;         /* [n_rep][bmax][9216]                                          */
-  float* w1_part;         /* [n_rep][bmax][2][MPLC_CNN_W1P] (per sample and row band)     */
+  float* w1_part;         /* [n_rep][bmax][MPLC_CNN_W1_BANDS][MPLC_CNN_W1P]: one [dW1 | db1]   */
+                          /* partial per sample and band of output tiles                    */
   float* w2_part;         /* [n_rep][w2_splits][MPLC_CNN_W2P]                             */
   float* w2t;             /* [n_rep][MPLC_CNN_W2T]: W2 in Winograd form for the forward   */
-                          /* conv, then W2 transposed for the data-gradient MFMA             */
+                          /* conv, then the rotated kernel's Winograd form for the dgrad     */
   /* optimizer (Keras 2.3.1 Adam) */
   float lr, beta1, beta2, eps;
   /* optional in-stream timing of one kernel of the step (bench roofline): hipEvent_t recorded right

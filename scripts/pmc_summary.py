@@ -21,3 +21,11 @@ for k, v in tot.items():
     print(f"{k[:44]:44s} {busy:9.3f} {v['SQ_INSTS_VALU'] / mf:9.2f} {v['SQ_LDS_BANK_CONFLICT'] / (v['SQ_LDS_IDX_ACTIVE'] + 1):8.3f} "
           f"{v['SQ_WAIT_INST_ANY'] / (v['SQ_ACTIVE_INST_ANY'] + 1):8.2f} {v['SQ_INSTS_VMEM_RD'] / mf:9.2f} "
           f"{2 * v['FETCH_SIZE'] / 1024 / 1024:9.2f}")
+
+# extra view: where the waves spend their cycles (SQ_WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY)
+print(f"\n{'kernel':44s} {'waves':>8s} {'wait_any':>8s} {'wait_ins':>8s} {'active':>8s} {'lds/mfma':>8s} {'ldswait':>8s}")
+for k, v in tot.items():
+    wc = v["SQ_WAVE_CYCLES"] + 1e-9
+    mf = v["SQ_INSTS_MFMA"] + 1e-9
+    print(f"{k[:44]:44s} {v['SQ_WAVES']:8.0f} {v['SQ_WAIT_ANY'] / wc:8.3f} {v['SQ_WAIT_INST_ANY'] / wc:8.3f} "
+          f"{v['SQ_ACTIVE_INST_ANY'] / wc:8.3f} {v['SQ_INSTS_LDS'] / mf:8.2f} {v['SQ_WAIT_INST_LDS'] / wc:8.3f}")
