@@ -975,54 +975,40 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv2 weight gradient: dW2[kyx*32+ci][co] = sum_px a1[py+ky][px+kx][ci] dZ2[px][co]; db2.
-// Block = (split s, replica r): samples [8s, 8s+8); 4 waves (one per SIMD), the 288 x 64 output split by
-// area: wave w owns rows [144*(w>>1), +144) (9 tiles of 16 = (kyx, ci half)) x cols [32*(w&1), +32) on
-// v_mfma_f32_16x16x4_f32 (72 accumulator registers).  Per k-step of 4 pixels a wave reads 9 A and 2 B
-// operands for 18 MFMAs.  Both operands are staged in LDS as [half|quarter][pixel][16] planes, so every
-// ds_read_b32 is one contiguous 64-lane run (conflict-free) and the lane offset is the lane id.
-// Per band of 4 conv2 rows: conv1 rows recomputed on MFMA (conv1_mfma) into LDS, dZ2 un-pooled from the
-// prefetched (dp, code) registers; the K loop over the band's 96 pixels is fully unrolled (compile-time
-// LDS offsets).  The next band's (dp, code) are fetched while the current band's MFMAs run.
-// Each output element is still one k-ordered f32 FMA chain over the split's pixels (sample, band, pixel).
+// conv2 weight gradient in Winograd form F(3x3, 2x2): per 2x2 tile of dZ2 (= one pooling window) and the
+// 4x4 conv1 patch it sees,  dW2[3x3] += G^T [ (A delta A^T) (.) (B^T d B) ] G  (the transposed dual of the
+// forward's F(2x2, 3x3); A, B, G are the forward's matrices).  The sum over tiles runs in the transformed
+// domain: 16 GEMMs M[xi][ci][co] = sum_tiles V[xi][tile][ci] D[xi][tile][co], then one inverse transform per
+// split: 2.25x fewer multiply-adds than the direct sum (16 per tile instead of 4 positions x 9 taps).
+// delta is the max-pool gradient of one window: a single nonzero v at the argmax (dy, dx) when positive,
+// so D = v * A[:, dy] (x) A[:, dx] is a sign pattern of v.
+// Block = (split s, replica r): samples [8s, 8s+8); 4 waves, wave i owns transform row i (xi = 4i .. 4i+3) x
+// 32 ci x 64 co (32 accumulators of v_mfma_f32_16x16x4_f32).  The work is a stream of bands (sample, 2 window
+// rows = 24 tiles): conv1 rows recomputed on MFMA (conv1_mfma, bit-identical to the forward's activations)
+// and the windows' (value, argmax) staged in LDS; per k-step of 4 tiles a lane forms 8 values of V (its
+// tile, two ci) and 16 of D (its tile, four co), for 32 MFMAs.  At the end the waves fold their row of the
+// inverse transform (P_i = M_i G) and exchange it through LDS.  Fixed-order sums: independent of which
+// other replicas share the launch.
 // ------------------------------------------------------------------------------------------------
-constexpr int WG_NC = 2;                  // 16-col tiles per wave (4 / WG_NC waves per row half)
-constexpr int WG_WAVES = 8 / WG_NC;
-constexpr int WG_THREADS = 64 * WG_WAVES;
-constexpr int WG_SAMPLES = 8;             // samples per wgrad split (fixed: reproducible sums)
-constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // pooled pairs per thread per band: 2 rows x 12 x 64
-constexpr int WG_A1H = 6 * A1 * 16 + 16;  // one ci-half plane of the band's conv1 rows (+16: write banks)
-constexpr int WG_DZQ = 4 * Z2 * 16 + 16;  // one co-quarter plane of the band's dense dZ2 (+16: write banks)
+constexpr int WG_THREADS = 256;
+constexpr int WG_SAMPLES = 8;                     // samples per wgrad split (fixed: reproducible sums)
+constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // (dp, code) pairs per thread per band: 2 rows x 12 x 64
+constexpr int WG_CS = 40;                         // a1 column stride (32 channels + pad: a tile step = 16 banks)
+constexpr int WG_A1 = 6 * A1 * WG_CS;             // one band's conv1 rows [6][26][40]
+constexpr int WG_VS = 80;                         // window stride of the staged dZ2 values (floats)
+constexpr int WG_SS = 80;                         // window stride of the staged argmax codes (bytes)
+constexpr int WG_PX = 3 * 16 * C2 + 16;           // one wave's P_i for one ci half: [3][16 ci][64 co] (+pad)
 
-// K loop over one band's 96 conv2 pixels, four per MFMA (px = 4*s4 + (lane >> 4)), for row half RH
-// (compile-time, so every LDS offset is an immediate).
-template <int RH>
-__device__ __forceinline__ void wgrad_band(const float* abase, const float* zb, fvec4 (&acc)[9][WG_NC]) {
-#pragma unroll
-  for (int s4 = 0; s4 < 24; ++s4) {
-    const int oyl = (4 * s4) / Z2, ox0 = (4 * s4) % Z2;
-    float b[WG_NC];
-#pragma unroll
-    for (int c = 0; c < WG_NC; ++c) b[c] = zb[c * WG_DZQ + (oyl * Z2 + ox0) * 16];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int t = 9 * RH + i;  // 16-row tile: kyx = t >> 1, ci half t & 1
-      const int kyx = t >> 1;
-      const float a = abase[(t & 1) * WG_A1H + ((oyl + kyx / 3) * A1 + ox0 + kyx % 3) * 16];
-#pragma unroll
-      for (int c = 0; c < WG_NC; ++c) acc[i][c] = mfma16(a, b[c], acc[i][c]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(WG_WAVES / 2, WG_WAVES / 2))) void conv_wgrad_kernel(
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
+  __shared__ float smem[(WG_A1 + 24 * WG_VS > 4 * WG_PX) ? WG_A1 + 24 * WG_VS : 4 * WG_PX];
+  __shared__ uint8_t sel_s[24 * WG_SS];
   __shared__ float img_s[IMG * IMG];
-  __shared__ float a1_s[2 * WG_A1H];
-  __shared__ float dzd_s[4 * WG_DZQ];
-  __shared__ float gb_s[WG_WAVES][C2];
+  __shared__ float gb_s[4][C2];
+  float* const a1_s = smem;            // [6][26][WG_CS]
+  float* const vq_s = smem + WG_A1;    // [24 windows][WG_VS]
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -1035,21 +1021,13 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(WG_W
   const int lane = tid & 63, wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
-  const int rh = wave / (4 / WG_NC);  // row half: 16-row tiles 9*rh .. 9*rh+8
-  const int ch = wave % (4 / WG_NC);  // col group: co quarters WG_NC*ch .. +WG_NC-1
   const float* P = params + (int64_t)r * stride;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
-  fvec4 acc[9][WG_NC];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-#pragma unroll
-    for (int c = 0; c < WG_NC; ++c) acc[i][c] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  }
-  float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread un-pools has that channel)
+  float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread stages has that channel)
   float pdv[WG_PRE];
   uint32_t pcd[WG_PRE];
-  // pooled rows 2*band, 2*band+1 of sample jj: pair e = tid + 256*s is element 24*64*band + e (contiguous)
+  // window rows 2*band, 2*band+1 of sample jj: pair e = tid + 256*s is element 24*64*band + e (contiguous)
   auto fetch = [&](int jj, int band) {
     const int64_t base = ((int64_t)r * bmax + jj) * FEAT + band * 2 * PL * C2;
 #pragma unroll
@@ -1059,7 +1037,6 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(WG_W
       pcd[s] = code[base + e];
     }
   };
-  // the sample's image is fetched into registers one sample ahead (with its dataset row index)
   constexpr int IMG_PRE = (IMG * IMG + WG_THREADS - 1) / WG_THREADS;
   float imgv[IMG_PRE];
   auto fetch_img = [&](int jj) {
@@ -1070,76 +1047,141 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(WG_W
       imgv[k] = xr[e < IMG * IMG ? e : 0];
     }
   };
+  // GEMM roles: wave = transform row i; lane (tl = lane & 15: ci / co in a group of 16, kq = lane >> 4: tile)
+  const int wi = wave;
+  const int tl = lane & 15, kq = lane >> 4;
+  // B^T row i (input transform) combines patch rows (ra, rb) with signs (sa, sb); A row i (gradient
+  // transform) picks delta's row dy with factor A[i][dy]
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  const float ai0 = (wi == 3) ? 0.0f : 1.0f;                       // A[i][0]
+  const float ai1 = (wi == 0) ? 0.0f : ((wi == 1) ? 1.0f : -1.0f);  // A[i][1]
+  fvec4 acc[4][2][4];  // [j][ci half][co group]
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fetch(j_begin, 0);
   fetch_img(j_begin);
-  // operand planes: lane l reads pixel (k-step base + (l >> 4)), row/col (l & 15) -> plane offset l
-  const float* zb = dzd_s + (WG_NC * ch) * WG_DZQ + lane;
-  const float* abase = a1_s + lane;
   for (int j = j_begin; j < j_end; ++j) {
-#pragma unroll
-    for (int k = 0; k < IMG_PRE; ++k)
-      if (tid + WG_THREADS * k < IMG * IMG) img_s[tid + WG_THREADS * k] = imgv[k];
     for (int band = 0; band < 6; ++band) {
-      __syncthreads();  // img_s loaded; previous band's MFMA readers done
+      __syncthreads();  // previous band's readers (a1_s, vq_s, sel_s; and img_s by its staging) done
+      if (band == 0) {
+#pragma unroll
+        for (int k = 0; k < IMG_PRE; ++k)
+          if (tid + WG_THREADS * k < IMG * IMG) img_s[tid + WG_THREADS * k] = imgv[k];
+        if (j + 1 < j_end) fetch_img(j + 1);
+        __syncthreads();
+      }
+      // windows of the band: (value masked by the positive bit, argmax)
 #pragma unroll
       for (int s = 0; s < WG_PRE; ++s) {
-        const int e = tid + WG_THREADS * s;
-        const int co = e & 63;
-        const int pc = (e >> 6) % PL;
-        const int prr = e / (PL * C2);
+        const int e = tid + WG_THREADS * s;  // window e >> 6 of the band (row-major), channel e & 63
         const uint32_t c = pcd[s];
         const float v = (c & 0x80) ? pdv[s] : 0.0f;
         gb += v;
-        const int sel = c & 3;
-        float* d = dzd_s + (co >> 4) * WG_DZQ + (co & 15);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[((2 * prr + (q >> 1)) * Z2 + 2 * pc + (q & 1)) * 16] = (sel == q) ? v : 0.0f;
+        vq_s[(e >> 6) * WG_VS + (e & 63)] = v;
+        sel_s[(e >> 6) * WG_SS + (e & 63)] = (uint8_t)(c & 3);
       }
       // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles of 32 over the block's waves
 #pragma unroll
-      for (int u = 0; u < (5 + WG_WAVES - 1) / WG_WAVES; ++u) {
-        const int t = wave + WG_WAVES * u;
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave + 4 * u;
         if (t < 5) {
           const int p = min(t * 32 + m, 6 * A1 - 1);
           const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
-          float* dst = a1_s + (m >> 4) * WG_A1H + (m & 15);
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) {
-            const int pw = t * 32 + acc_row(reg, kh);
-            if (pw < 6 * A1) dst[pw * 16] = fmaxf(a[reg], 0.0f);
+            const int pw = min(t * 32 + acc_row(reg, kh), 6 * A1 - 1);  // clamped rows rewrite row 155's value
+            a1_s[pw * WG_CS + m] = fmaxf(a[reg], 0.0f);
           }
         }
       }
-      if (band < 5) {
-        fetch(j, band + 1);
-      } else if (j + 1 < j_end) {
-        fetch(j + 1, 0);
-        fetch_img(j + 1);
-      }
+      if (band < 5) fetch(j, band + 1);
+      else if (j + 1 < j_end) fetch(j + 1, 0);
       __syncthreads();
-      if (rh == 0) wgrad_band<0>(abase, zb, acc);
-      else wgrad_band<1>(abase, zb, acc);
+      // 6 k-steps of 4 tiles (window (wr, wc) = tile 12*wr + wc of the band; lane kq takes tile 4*st + kq)
+#pragma unroll 1
+      for (int st = 0; st < 6; ++st) {
+        const int tb = 4 * st + kq;
+        const int wr = tb / PL, wc = tb % PL;
+        // V: B^T d B of the tile's 4x4 conv1 patch (rows 2*wr .., columns 2*wc ..), channels tl, 16 + tl
+        const float* d0 = a1_s + ((2 * wr + ra) * A1 + 2 * wc) * WG_CS + tl;
+        const int drow = (rb - ra) * A1 * WG_CS;
+        float va[2][4];
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+          float t[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * WG_CS + 16 * ch] + sb * d0[drow + c * WG_CS + 16 * ch];
+          va[ch][0] = t[0] - t[2];
+          va[ch][1] = t[1] + t[2];
+          va[ch][2] = t[2] - t[1];
+          va[ch][3] = t[1] - t[3];
+        }
+        // D: delta's single nonzero v at (dy, dx): D[i][j] = v * A[i][dy] * A[j][dx], channels 16*cg + tl
+        float db[4][4];
+#pragma unroll
+        for (int cg = 0; cg < 4; ++cg) {
+          const float v = vq_s[tb * WG_VS + 16 * cg + tl];
+          const int sl = sel_s[tb * WG_SS + 16 * cg + tl];
+          const float vi = ((sl & 2) ? ai1 : ai0) * v;
+          const bool dx = (sl & 1) != 0;
+          db[cg][0] = dx ? 0.0f : vi;
+          db[cg][1] = vi;
+          db[cg][2] = dx ? -vi : vi;
+          db[cg][3] = dx ? -vi : 0.0f;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+            for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = mfma16(va[ch][jj], db[cg][jj], acc[jj][ch][cg]);
+      }
     }
-    __syncthreads();  // last band's readers done before the next sample's img_s load
   }
+  // inverse transform dW2[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]: wave i folds
+  // its row (P_i0 = M_i0 + .5 M_i1 + .5 M_i2, P_i1 = .5 M_i1 - .5 M_i2, P_i2 = .5 M_i1 + .5 M_i2 + M_i3), the
+  // waves exchange P through LDS, one ci half at a time.  Lane holds ci 16*ch + 4*kq + rr, co 16*cg + tl.
+  gb_s[wave][lane] = gb;
   float* out = w2_part + ((int64_t)r * splits + sp) * MPLC_CNN_W2P;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int row0 = 16 * (9 * rh + i) + 4 * (lane >> 4);  // row = kyx*32 + ci
+  for (int ch = 0; ch < 2; ++ch) {
+    __syncthreads();  // previous readers of smem (the last band, or the previous half) done
+    float* px = smem + wi * WG_PX;
 #pragma unroll
-    for (int c = 0; c < WG_NC; ++c) {
+    for (int cg = 0; cg < 4; ++cg)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) out[(row0 + rr) * C2 + 16 * (WG_NC * ch + c) + (lane & 15)] = acc[i][c][rr];
+      for (int rr = 0; rr < 4; ++rr) {
+        const float m0 = acc[0][ch][cg][rr], m1 = acc[1][ch][cg][rr], m2 = acc[2][ch][cg][rr],
+                    m3 = acc[3][ch][cg][rr];
+        const int o = (4 * kq + rr) * C2 + 16 * cg + tl;
+        px[o] = (m0 + 0.5f * m1) + 0.5f * m2;
+        px[16 * C2 + o] = 0.5f * m1 - 0.5f * m2;
+        px[32 * C2 + o] = (0.5f * m1 + 0.5f * m2) + m3;
+      }
+    __syncthreads();
+    for (int e = tid; e < 16 * C2; e += WG_THREADS) {  // (ci in half, co)
+      const int ci = 16 * ch + (e >> 6), co = e & 63;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float p0 = smem[0 * WG_PX + kx * 16 * C2 + e], p1 = smem[1 * WG_PX + kx * 16 * C2 + e];
+        const float p2 = smem[2 * WG_PX + kx * 16 * C2 + e], p3 = smem[3 * WG_PX + kx * 16 * C2 + e];
+        const float w0 = (p0 + 0.5f * p1) + 0.5f * p2;
+        const float w1 = 0.5f * p1 - 0.5f * p2;
+        const float w2 = (0.5f * p1 + 0.5f * p2) + p3;
+        out[((0 * 3 + kx) * C1 + ci) * C2 + co] = w0;
+        out[((1 * 3 + kx) * C1 + ci) * C2 + co] = w1;
+        out[((2 * 3 + kx) * C1 + ci) * C2 + co] = w2;
+      }
     }
   }
-  gb_s[wave][lane] = gb;
-  __syncthreads();
-  if (tid < C2) {
-    float g = 0.0f;
-#pragma unroll
-    for (int w = 0; w < WG_WAVES; ++w) g += gb_s[w][tid];
-    out[9 * C1 * C2 + tid] = g;
-  }
+  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + (gb_s[2][tid] + gb_s[3][tid]);
 }
 
 // Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
