@@ -710,7 +710,8 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
 
 // W2 for the data gradient in Winograd form: the data gradient is the correlation of the padded dZ2 with
 // the kernel rotated by 180 degrees and its channels swapped, W2r[ky][kx][co][ci] = W2[2-ky][2-kx][ci][co];
-// Ur[xi = 4i + j][co][ci] = (G W2r G^T)[i][j]  (ci contiguous: the B operand of the dgrad GEMMs).
+// Ur[co][ci][xi = 4i + j] = (G W2r G^T)[i][j]: the 16 transform points of one (co, ci) pair are contiguous, so
+// conv_bwd_data stages a channel quarter with 16-byte copies and a lane reads its 16 B operands as 4 x b128.
 __global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restrict__ params, int64_t stride,
                                                            const int32_t* __restrict__ cnt, float* __restrict__ Ur) {
   const int r = blockIdx.y;
@@ -733,51 +734,56 @@ __global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
   }
-  float* U = Ur + (int64_t)r * MPLC_CNN_W2T + e;
+  fvec4* U = reinterpret_cast<fvec4*>(Ur + (int64_t)r * MPLC_CNN_W2T + (int64_t)e * 16);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float o[4];
     wino_g_rows(gg[i], o);
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) U[(4 * i + jj) * C1 * C2] = o[jj];
+    U[i] = fvec4{o[0], o[1], o[2], o[3]};
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv2 data gradient + conv1 backward, Winograd F(2x2, 3x3).  Block = (band of 48 output tiles, sample,
-// replica), 4 waves.  dA1[y][x][ci] = sum_{ky,kx,co} dZ2p[y+ky][x+kx][co] W2r[ky][kx][co][ci] (dZ2p = dZ2
-// padded by 2): 13 x 13 output tiles of 2x2 in row-major order, 16 GEMMs M[xi][tile][ci] = sum_co
-// V[xi][tile][co] Ur[xi][co][ci], K = 64 output channels of conv2.
-// The band's rows of dZ2 (the max-pool gradient: one nonzero per window, at its argmax when positive) are
-// un-pooled from (dp, code) into a dense LDS tile one quarter of the channels (16) at a time, with zero
-// rows / columns around the 12 x 12 grid, so a tile's 4x4 patch is read without tests.  Wave i owns
-// transform row i (xi = 4i .. 4i+3) of the band's three 16-tile groups x both 16-channel halves of ci
-// (24 accumulators of v_mfma_f32_16x16x4_f32): per k-step a lane reads 2 patch rows (8 values), forms its
-// 4 values of V with 8 adds, and issues 24 MFMAs with 8 B operands (Ur, L2-resident) loaded one k-step
-// ahead.  Epilogue per group: each wave folds its row of the output transform into LDS; then every wave takes
-// 4 tiles (16 positions): dA1 = sum_i A^T T_i, dZ1 = dA1 * ReLU'(conv1) (conv1 recomputed on MFMA by
-// conv1_mfma, bit-identical to the forward's), and [dW1 | db1] += patch^T dZ1 on MFMA (rows = 9 taps + bias);
-// one partial per (sample, band), the waves' partials added in a fixed order.
+// conv2 data gradient + conv1 backward, Winograd F(2x2, 3x3).  dA1[y][x][ci] = sum_{ky,kx,co} dZ2p[y+ky][x+kx][co]
+// W2r[ky][kx][co][ci] (dZ2p = dZ2 padded by 2) over 13 x 13 output tiles of 2x2 (row-major), as 16 GEMMs
+// M[xi][tile][ci] = sum_co V[xi][tile][co] Ur[xi][co][ci], V = B^T d B of the tile's 4x4 dZ2p patch, K = 64.
+// Block = (band of 64 tiles, sample, replica), 4 waves; wave w owns tiles 16w .. 16w+15 of the band and ALL 16
+// transform points for both 16-channel halves of ci (32 accumulators of v_mfma_f32_16x16x4_f32).  Per k-step
+// (4 output channels of conv2) a lane reads its tile's 4x4 patch at one channel (16 LDS reads), forms the 16
+// values of V with 32 adds and issues 32 MFMAs with B operands read from the staged Ur quarter (4 x b128 per
+// half): half an LDS read per MFMA (a wave per transform row read one per MFMA: 55 % MFMA issue).
+// dZ2 (the max-pool gradient: one nonzero per window, at its argmax when positive) is un-pooled from
+// (dp, code) into a dense LDS band one quarter of the channels (16) at a time, with zero rows / columns around
+// the 12 x 12 grid, so a patch is read without tests; Ur's quarter is staged beside it, its 4 chunks of 4
+// transform points XOR-swizzled by ci so that the b128 reads of a lane group hit 64 distinct banks.
+// Epilogue, wave-local: the output transform Y = A^T M A of each (tile, ci) in registers; conv1's
+// pre-activation at the same positions recomputed on 16x16x4 MFMAs in the accumulator layout (taps 0..8 and
+// the bias in the order of conv1_mfma, so the ReLU' mask is the forward's); dZ1 = Y * ReLU'; [dW1 | db1] +=
+// patch^T dZ1 on 16x16x4 MFMAs whose B operand is dZ1 straight from registers.  One partial per (sample,
+// band), the waves' partials added in a fixed order.
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_THREADS = 256;
 constexpr int BWD_TILES = 169;                 // 13 x 13 output tiles of 2 x 2 over the 26 x 26 conv1 grid
-constexpr int BWD_BAND_TILES = 48;             // tiles per block (3 groups of 16)
-constexpr int BWD_BANDS = 4;                   // ceil(169 / 48)
-constexpr int BWD_WR = 6;                      // window rows a band's patches touch (tile rows + 1)
+constexpr int BWD_BAND_TILES = 64;             // tiles per block (one 16-tile group per wave)
+constexpr int BWD_BANDS = MPLC_CNN_W1_BANDS;   // ceil(169 / 64) = 3
+constexpr int BWD_WR = 7;                      // window rows a band's patches touch (<= 6 tile rows + 1)
 constexpr int BWD_DR = 2 * BWD_WR;             // dZ2 rows staged
 constexpr int BWD_DC = Z2 + 4;                 // dZ2 columns staged: 2 zero columns each side
 constexpr int BWD_CS = 17;                     // channel stride (16 channels of a quarter + 1: bank spread)
-constexpr int BWD_TS = C1 + 1;                 // tile stride of a T plane (odd: conflict-free writes)
-constexpr int BWD_TQ = 16 * BWD_TS;            // one (row i, b) plane of T for a 16-tile group
-constexpr int BWD_PRE = (BWD_WR * PL * 16 + BWD_THREADS - 1) / BWD_THREADS;  // (dp, code) pairs per thread
+constexpr int BWD_RS = BWD_DC * BWD_CS;        // staged row stride
+constexpr int BWD_PAIRS = BWD_WR * PL * 16;    // (dp, code) pairs of a quarter
+constexpr int BWD_PRE = (BWD_PAIRS + BWD_THREADS - 1) / BWD_THREADS;
+constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quarter [co 16][ci 32][xi 16]
+static_assert(BWD_BANDS * BWD_BAND_TILES >= BWD_TILES && (BWD_BANDS - 1) * BWD_BAND_TILES < BWD_TILES,
+              "MPLC_CNN_W1_BANDS must be ceil(169 / 64)");
 
 __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_bwd_data_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     const float* __restrict__ params, int64_t stride, const float* __restrict__ Ur,
     const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
-  __shared__ float dz_s[BWD_DR * BWD_DC * BWD_CS];
+  __shared__ float dz_s[BWD_DR * BWD_RS];
+  __shared__ fvec4 ur_s[BWD_UQ / 4];
   __shared__ float img_s[IMG * IMG];
-  __shared__ float t_s[8 * BWD_TQ];
   __shared__ float red_s[4][10 * 32];
   const int64_t lb = xcd_block();  // logical block (band, j, r), replica-major
   const int band = (int)(lb % BWD_BANDS);
@@ -785,14 +791,18 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   const int r = (int)(lb / ((int64_t)BWD_BANDS * gridDim.y));
   if (j >= cnt[r]) return;
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int tl = lane & 15, kq = lane >> 4;
   const int row = idx[(int64_t)r * bmax + j];
   const float* P = params + (int64_t)r * stride;
   const int tile0 = band * BWD_BAND_TILES;
-  const int ngroups = min(3, (BWD_TILES - tile0 + 15) / 16);
   const int ty0 = tile0 / 13;
   const int wy0 = ty0 - 1;  // first window row staged (local window row 0; rows outside 0..11 stay zero)
+  const int gt0 = tile0 + 16 * wave;         // this wave's first tile
+  const bool active = gt0 < BWD_TILES;       // wave-uniform: the last band's last wave has no tile
   const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
   const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
+  const fvec4* Uq = reinterpret_cast<const fvec4*>(Ur + (int64_t)r * MPLC_CNN_W2T);
   // pair e of a quarter: channel e & 15, window column (e >> 4) % 12, local window row e / 192
   float pdv[BWD_PRE];
   uint32_t pcd[BWD_PRE];
@@ -801,7 +811,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     for (int s = 0; s < BWD_PRE; ++s) {
       const int e = tid + BWD_THREADS * s;
       const int wy = wy0 + e / (PL * 16);
-      const bool ok = e < BWD_WR * PL * 16 && wy >= 0 && wy < PL;
+      const bool ok = e < BWD_PAIRS && wy >= 0 && wy < PL;
       const int pidx = (wy * PL + (e >> 4) % PL) * C2 + 16 * q + (e & 15);
       pdv[s] = ok ? dp[pidx] : 0.0f;
       pcd[s] = ok ? cd[pidx] : 0u;
@@ -826,147 +836,158 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       dz_s[(rr * BWD_DC + (c < 2 ? c : BWD_DC - 4 + c)) * BWD_CS + k] = 0.0f;
     }
   }
-  const int lane = tid & 63, wave = tid >> 6;
-  const int n = lane & 31;
-  const int kh = lane >> 5;
-  float w1r[5];
-  load_w1r(P, kh, n, w1r);
-  // GEMM roles: wave = transform row i; lane (tl = lane & 15: tile in group / ci in half, kq = lane >> 4)
-  const int wi = wave;
-  const int tl = lane & 15, kq = lane >> 4;
-  // B^T row i combines patch rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  int pa[3];  // this lane's patch origin (staged row 2*(ty - ty0) + ra, column 2*tx) per group, + channel kq
+  // A operand (V): this lane's tile tl of the wave's group at channel kq of each k-step
+  const int tcl = min(gt0 + tl, BWD_TILES - 1);
+  const int pa = ((2 * (tcl / 13 - ty0)) * BWD_DC + 2 * (tcl % 13)) * BWD_CS + kq;
+  // B operand (Ur): ci = 16h + tl, co = 4st + kq of the quarter; chunk m of the 16 transform points at
+  // m ^ swz (the staging applies the same XOR)
+  const int swz = (tl >> 2) & 3;
+  fvec4 acc[16][2];  // [xi][ci half]
 #pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    const int t = min(tile0 + 16 * g + tl, BWD_TILES - 1);
-    const int ty = t / 13, tx = t % 13;
-    pa[g] = ((2 * (ty - ty0) + ra) * BWD_DC + 2 * tx) * BWD_CS + kq;
-  }
-  const int drow = (rb - ra) * BWD_DC * BWD_CS;
-  const float* Ub = Ur + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C2 * C1 + kq * C1 + tl;
-  auto load_b = [&](int k4, float (&bv)[8]) {  // k4: global k-step (channels 4*k4 .. 4*k4+3)
+  for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int ch = 0; ch < 2; ++ch) bv[2 * jj + ch] = Ub[(int64_t)jj * C2 * C1 + (4 * k4) * C1 + 16 * ch];
-  };
-  fvec4 acc[3][4][2];  // [group][j][ci half]
-#pragma unroll
-  for (int g = 0; g < 3; ++g)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int ch = 0; ch < 2; ++ch) acc[g][jj][ch] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  float bcur[8], bnxt[8];
-  load_b(0, bcur);
+    for (int h = 0; h < 2; ++h) acc[xi][h] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 1
   for (int q = 0; q < 4; ++q) {  // channel quarters
     __syncthreads();             // previous quarter's readers done (and the zero columns / image written)
+    {
+      constexpr int UIT = BWD_UQ / 4 / BWD_THREADS;  // 8 chunks of 4 floats per thread
+      fvec4 uv[UIT];  // the quarter's Ur: loads in flight while the band is un-pooled
 #pragma unroll
-    for (int s = 0; s < BWD_PRE; ++s) {  // un-pool the quarter's (dp, code) into the dense band
-      const int e = tid + BWD_THREADS * s;
-      if (e < BWD_WR * PL * 16) {
-        const int lwy = e / (PL * 16), wx = (e >> 4) % PL, ch = e & 15;
-        const uint32_t c = pcd[s];
-        const float v = (c & 0x80) ? pdv[s] : 0.0f;
-        const int sel = c & 3;
-        float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
-        d[0] = (sel == 0) ? v : 0.0f;
-        d[BWD_CS] = (sel == 1) ? v : 0.0f;
-        d[BWD_DC * BWD_CS] = (sel == 2) ? v : 0.0f;
-        d[BWD_DC * BWD_CS + BWD_CS] = (sel == 3) ? v : 0.0f;
+      for (int s = 0; s < UIT; ++s) uv[s] = Uq[q * (BWD_UQ / 4) + tid + BWD_THREADS * s];
+#pragma unroll
+      for (int s = 0; s < BWD_PRE; ++s) {  // un-pool the quarter's (dp, code) into the dense band
+        const int e = tid + BWD_THREADS * s;
+        if (e < BWD_PAIRS) {
+          const int lwy = e / (PL * 16), wx = (e >> 4) % PL, ch = e & 15;
+          const uint32_t c = pcd[s];
+          const float v = (c & 0x80) ? pdv[s] : 0.0f;
+          const int sel = c & 3;
+          float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
+          d[0] = (sel == 0) ? v : 0.0f;
+          d[BWD_CS] = (sel == 1) ? v : 0.0f;
+          d[BWD_DC * BWD_CS] = (sel == 2) ? v : 0.0f;
+          d[BWD_DC * BWD_CS + BWD_CS] = (sel == 3) ? v : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < UIT; ++s) {  // chunk k = (co, ci, m): stored at m ^ ((ci >> 2) & 3)
+        const int k = tid + BWD_THREADS * s;
+        const int pair = k >> 2, m = k & 3;
+        ur_s[pair * 4 + (m ^ ((pair >> 2) & 3))] = uv[s];
       }
     }
     if (q < 3) fetch(q + 1);
     __syncthreads();
+    if (active) {
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int k4 = 4 * q + st;
-      if (k4 + 1 < 16) load_b(k4 + 1, bnxt);
+      for (int st = 0; st < 4; ++st) {
+        // B operands first (independent of V): Ur[xi][4st + kq][16h + tl], 4 x b128 per half
+        fvec4 b[2][4];
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const float* d0 = dz_s + pa[g] + 4 * st;
-        float t[4];
+        for (int h = 0; h < 2; ++h) {
+          const fvec4* ub = ur_s + ((4 * st + kq) * C1 + 16 * h + tl) * 4;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * BWD_CS] + sb * d0[drow + c * BWD_CS];
-        float v4[4];
-        v4[0] = t[0] - t[2];
-        v4[1] = t[1] + t[2];
-        v4[2] = t[2] - t[1];
-        v4[3] = t[1] - t[3];
+          for (int m = 0; m < 4; ++m) b[h][m] = ub[m ^ swz];
+        }
+        // V = B^T d B of the 4x4 patch (rows r, columns c) at channel 4st + kq
+        const float* d0 = dz_s + pa + 4 * st;
+        float t[4][4];  // t[i][c] = (B^T d)[i][c]
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
+        for (int c = 0; c < 4; ++c) {
+          const float d_0 = d0[c * BWD_CS], d_1 = d0[BWD_RS + c * BWD_CS];
+          const float d_2 = d0[2 * BWD_RS + c * BWD_CS], d_3 = d0[3 * BWD_RS + c * BWD_CS];
+          t[0][c] = d_0 - d_2;
+          t[1][c] = d_1 + d_2;
+          t[2][c] = d_2 - d_1;
+          t[3][c] = d_1 - d_3;
+        }
+        float v[16];
 #pragma unroll
-          for (int ch = 0; ch < 2; ++ch) acc[g][jj][ch] = mfma16(v4[jj], bcur[2 * jj + ch], acc[g][jj][ch]);
-      }
-      if (k4 + 1 < 16) {
+        for (int i = 0; i < 4; ++i) {
+          v[4 * i + 0] = t[i][0] - t[i][2];
+          v[4 * i + 1] = t[i][1] + t[i][2];
+          v[4 * i + 2] = t[i][2] - t[i][1];
+          v[4 * i + 3] = t[i][1] - t[i][3];
+        }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) bcur[k] = bnxt[k];
+        for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[xi][h] = mfma16(v[xi], b[h][xi >> 2][xi & 3], acc[xi][h]);
       }
     }
   }
-  const int toff = (n < 9) ? (n / 3) * IMG + n % 3 : 0;  // dW1 A operand: tap n of a position
-  floatx16 gacc = zero16();                              // [dW1 | db1] partial: rows = tap, cols = ci
+  // ---- epilogue (wave-local).  Lane (tl, kq) holds M[xi][tile 4kq + rr][ci 16h + tl] in acc[xi][h][rr].
+  // conv1 weights as the B operand of the 16x16x4 recompute: W1e[4s + kq][16h + tl], rows 0..8 = taps, 9 = bias
+  float w1b[3][2];
 #pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    if (g >= ngroups) break;
-    __syncthreads();  // previous group's T readers done
-    // T_i[b] = sum_j M_ij A[j][b] into LDS: lane holds tiles 4*kq + rr of the group, ci 16*ch + tl
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float m0 = acc[g][0][ch][rr], m1 = acc[g][1][ch][rr], m2 = acc[g][2][ch][rr], m3 = acc[g][3][ch][rr];
-        const int o = (4 * kq + rr) * BWD_TS + 16 * ch + tl;
-        t_s[(2 * wi) * BWD_TQ + o] = (m0 + m1) + m2;
-        t_s[(2 * wi + 1) * BWD_TQ + o] = (m1 - m2) - m3;
-      }
-    __syncthreads();
-    // wave w takes tiles 4w .. 4w+3 of the group = 16 positions m = 4*(tile) + q (q = 2dy+dx); conv1_mfma
-    // rows m (lanes 0-15 of each half; rows 16-31 repeat them and are not used)
-    const int m = n & 15;
-    const int tq = tile0 + 16 * g + 4 * wave + (m >> 2);
-    const int tqc = min(tq, BWD_TILES - 1);
-    const int py = 2 * (tqc / 13) + ((m & 3) >> 1), px = 2 * (tqc % 13) + (m & 1);
-    const floatx16 a1 = conv1_mfma(img_s, py * IMG + px, kh, w1r);
-    // lane (n = ci, kh) holds positions acc_row(reg, kh): reg 0..3 -> tile kh, q = reg; reg 4..7 -> tile 2+kh
+  for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int tg = 4 * wave + 2 * h + kh;  // tile within the group
-      const int tt = tile0 + 16 * g + tg;
-      float tv[4][2];
+      const int k = 4 * s3 + kq, ci = 16 * h + tl;
+      w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
+    }
+  fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
+  fvec4 gacc1 = gacc;
+  if (active) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int rr = 0; rr < 4; ++rr) {
+      // positions of the MFMA rows m = 4 kq' + q: tile 4kq' + rr of the group, window pixel q = 2a + b
+      // A operands for this lane as a row (m = tl): its position's taps 4s + kq (conv1) ...
+      const int tA = min(gt0 + 4 * (tl >> 2) + rr, BWD_TILES - 1);
+      const int pyA = 2 * (tA / 13) + ((tl & 3) >> 1), pxA = 2 * (tA % 13) + (tl & 1);
+      float a1v[3];
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * BWD_TQ + tg * BWD_TS + n];
-      float y[4];
-      y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
-      y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
-      y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
-      y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
-      const int ttc = min(tt, BWD_TILES - 1);
-      const bool valid = tt < BWD_TILES && tt < tile0 + BWD_BAND_TILES;
+      for (int s3 = 0; s3 < 3; ++s3) {
+        const int k = 4 * s3 + kq;
+        a1v[s3] = (k < 9) ? img_s[(pyA + k / 3) * IMG + pxA + k % 3] : ((k == 9) ? 1.0f : 0.0f);
+      }
+      // ... and as a K index (k = kq) for dW1: position (tile 4kq + rr, q), tap tl
+      const int tB = gt0 + 4 * kq + rr;
+      const bool valid = tB < BWD_TILES && tB < tile0 + BWD_BAND_TILES;
+      const int tBc = min(tB, BWD_TILES - 1);
+      fvec4 z[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        fvec4 c1 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) c1 = mfma16(a1v[s3], w1b[s3][h], c1);
+        // output transform of (tile 4kq + rr, ci 16h + tl): T_i = M_i A, Y = A^T T
+        float tv[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float m0 = acc[4 * i][h][rr], m1 = acc[4 * i + 1][h][rr], m2 = acc[4 * i + 2][h][rr],
+                      m3 = acc[4 * i + 3][h][rr];
+          tv[i][0] = (m0 + m1) + m2;
+          tv[i][1] = (m1 - m2) - m3;
+        }
+        float y[4];
+        y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
+        y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
+        y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
+        y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) z[h][qq] = (valid && c1[qq] > 0.0f) ? y[qq] : 0.0f;
+      }
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
-        const int reg = 4 * h + qq;
-        const float dz = (valid && a1[reg] > 0.0f) ? y[qq] : 0.0f;
-        // A operand: tap n (< 9) of this lane-half's position, 1 for the bias row
-        const int qy = 2 * (ttc / 13) + (qq >> 1), qx = 2 * (ttc % 13) + (qq & 1);
-        const float pv = img_s[qy * IMG + qx + toff];
-        const float av = (n < 10) ? (n < 9 ? pv : 1.0f) : 0.0f;
-        gacc = mfma32(av, dz, gacc);
+        // A: tap tl of position (tile 4kq + rr, q = qq); 1 for the bias row, 0 beyond
+        const int py = 2 * (tBc / 13) + (qq >> 1), px = 2 * (tBc % 13) + (qq & 1);
+        const float pv = (tl < 9) ? img_s[(py + tl / 3) * IMG + px + tl % 3] : 0.0f;
+        const float av = (tl < 9) ? pv : ((tl == 9) ? 1.0f : 0.0f);
+        gacc = mfma16(av, z[0][qq], gacc);
+        gacc1 = mfma16(av, z[1][qq], gacc1);
       }
     }
   }
-  // gacc: rows = tap (0..9), cols = ci; rows 0..9 live in regs 0..3 (kh 0: rows 0-3, kh 1: rows 4-7), 4..5 (kh 0)
+  // gacc / gacc1: rows = tap 4kq + reg (0..9 used), col = ci tl / 16 + tl
 #pragma unroll
-  for (int reg = 0; reg < 8; ++reg) {
-    const int k = acc_row(reg, kh);
-    if (k < 10) red_s[wave][k * 32 + n] = gacc[reg];
+  for (int reg = 0; reg < 4; ++reg) {
+    const int k = 4 * kq + reg;
+    if (k < 10) {
+      red_s[wave][k * 32 + tl] = gacc[reg];
+      red_s[wave][k * 32 + 16 + tl] = gacc1[reg];
+    }
   }
   __syncthreads();
   float* out = w1_part + (((int64_t)r * bmax + j) * BWD_BANDS + band) * MPLC_CNN_W1P;

@@ -26,7 +26,7 @@ FEAT = 9216
 HID = 128
 W1P = 320
 W2P = 18496
-W1_BANDS = 4  # MPLC_CNN_W1_BANDS: [dW1 | db1] partials per sample (data-gradient blocks)
+W1_BANDS = 3  # MPLC_CNN_W1_BANDS: [dW1 | db1] partials per sample (data-gradient blocks)
 W2T = 32768  # MPLC_CNN_W2T: W2 in Winograd form (forward), then transposed (data gradient)
 WG_SAMPLES = 8
 PATIENCE = 10

@@ -43,7 +43,7 @@ extern "C" {
 #define MPLC_CNN_OFF_B4 1199872    /* 10         */
 #define MPLC_CNN_NPARAM 1199882
 #define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
-#define MPLC_CNN_W1_BANDS 4        /* data-gradient blocks per sample (48 Winograd tiles each) */
+#define MPLC_CNN_W1_BANDS 3        /* data-gradient blocks per sample (64 Winograd tiles each) */
 #define MPLC_CNN_W2T 32768         /* per-model W2 workspace: 16 Winograd planes x 32 x 64 floats */
 #define MPLC_CNN_FEAT 9216         /* flattened pooled features */
 #define MPLC_CNN_HID 128
