@@ -44,9 +44,12 @@ for _p in (REPO, PKG):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (v_mfma_f32_32x32x2_f32), spec
-CONV_BWD_DATA_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2  # dA1 = dZ2 (*) W2 over all conv1 positions (direct conv)
-# the kernel computes it in Winograd form F(2x2,3x3): 169 output tiles x 16 transform points x 64 x 32 MACs
-CONV_BWD_DATA_WINOGRAD_FLOP_PER_SAMPLE = 169 * 16 * 64 * 32 * 2
+# conv2's data gradient per sample.  The kernel runs it in Winograd form F(2x2,3x3): 169 output tiles x 16
+# transform points x 64 x 32 multiply-adds, all fp32 - that algorithm's arithmetic is the roofline count.  The
+# direct convolution (every conv1 position x 32 x 576) is 2.25x more and is reported beside it only as the
+# equivalent rate: priced against the MFMA peak it would read as ~100 % while the matrix cores are half idle.
+CONV_BWD_DATA_FLOP_PER_SAMPLE = 169 * 16 * 64 * 32 * 2
+CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2
 MNIST_FWD_FLOP = 23984896       # per sample, SURVEY A21
 MNIST_TRAIN_FLOP = 71565312     # per sample (fwd + wgrad + dgrad, no conv1 dgrad)
 TRAFFIC_SOURCE = ("profiles/pmc_traffic.json: FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes of "
@@ -424,14 +427,13 @@ def bench_train(args, rank, world):
                      "kernel_ms_avg": round(kern_ms / max(1, launches), 4),
                      "algorithmic_flop_per_launch": int(flops / max(1, launches)),
                      "flop_per_sample": CONV_BWD_DATA_FLOP_PER_SAMPLE,
-                     # the algorithmic count is the direct convolution's; the kernel runs the same
-                     # math in Winograd form, whose own multiply-adds are 0.444 of it: its MFMA-executed rate is
-                     "winograd_flop_per_sample": CONV_BWD_DATA_WINOGRAD_FLOP_PER_SAMPLE,
-                     "winograd_executed_tflops": round(achieved * CONV_BWD_DATA_WINOGRAD_FLOP_PER_SAMPLE
-                                                       / CONV_BWD_DATA_FLOP_PER_SAMPLE, 2),
-                     "note": "achieved = direct-convolution FLOPs / kernel time (the contract's algorithmic "
-                             "count); the conv2 kernels use Winograd F(2x2,3x3) / F(3x3,2x2), 2.25x fewer "
-                             "multiply-adds, all in fp32"},
+                     "direct_conv_flop_per_sample": CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE,
+                     "direct_conv_equivalent_tflops": round(achieved * CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE
+                                                            / CONV_BWD_DATA_FLOP_PER_SAMPLE, 2),
+                     "note": "achieved = the Winograd F(2x2,3x3) algorithm's own fp32 multiply-adds (169 tiles x "
+                             "16 points x 64 x 32 per sample) / in-stream kernel time, i.e. how busy the matrix "
+                             "cores are; the direct convolution the reference computes is 2.25x more FLOPs "
+                             "(direct_conv_equivalent_tflops)"},
         "shapley_values": [round(float(v), 6) for v in c.contributivity_scores],
         # coalition evaluations as the reference counts them, and the realised epochs (fixed E,
         # early stopping off, so every coalition trains exactly E epochs)

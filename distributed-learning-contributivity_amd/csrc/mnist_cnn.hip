@@ -28,6 +28,7 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float fvec4 __attribute__((ext_vector_type(4)));
+typedef float fvec2 __attribute__((ext_vector_type(2)));
 
 constexpr int IMG = 28;
 constexpr int A1 = 26;
@@ -1014,22 +1015,24 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 constexpr int WG_THREADS = 256;
 constexpr int WG_SAMPLES = 8;                     // samples per wgrad split (fixed: reproducible sums)
 constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // (dp, code) pairs per thread per band: 2 rows x 12 x 64
-constexpr int WG_CS = 40;                         // a1 column stride (32 channels + pad: a tile step = 16 banks)
-constexpr int WG_A1 = 6 * A1 * WG_CS;             // one band's conv1 rows [6][26][40]
-constexpr int WG_VS = 80;                         // window stride of the staged dZ2 values (floats)
-constexpr int WG_SS = 80;                         // window stride of the staged argmax codes (bytes)
+// Staged operands are read as 8-byte pairs: a lane needs channels ci and 16 + ci of a conv1 position (stored
+// adjacent: slot 2 * (ci & 15) + (ci >> 4)) and (value, argmax) of a window channel (one int2), so a k-step's
+// 32 MFMAs take 12 ds_read_b64 instead of 24 4-byte reads.  The strides put the two lane halves of a b64 read
+// group (tiles kq, kq + 1: 2 positions or 1 window apart) on opposite halves of the 64 banks.
+constexpr int WG_CS = 48;                         // a1 position stride (32 channels + pad; 2 * 48 = 32 mod 64)
+constexpr int WG_A1 = 6 * A1 * WG_CS;             // one band's conv1 rows [6][26][48]
+constexpr int WG_VS = 80;                         // window stride of the staged (value, argmax) pairs (int2)
 constexpr int WG_PX = 3 * 16 * C2 + 16;           // one wave's P_i for one ci half: [3][16 ci][64 co] (+pad)
 
 __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
-  __shared__ float smem[(WG_A1 + 24 * WG_VS > 4 * WG_PX) ? WG_A1 + 24 * WG_VS : 4 * WG_PX];
-  __shared__ uint8_t sel_s[24 * WG_SS];
+  __shared__ float smem[(WG_A1 + 24 * WG_VS * 2 > 4 * WG_PX) ? WG_A1 + 24 * WG_VS * 2 : 4 * WG_PX];
   __shared__ float img_s[IMG * IMG];
   __shared__ float gb_s[4][C2];
   float* const a1_s = smem;            // [6][26][WG_CS]
-  float* const vq_s = smem + WG_A1;    // [24 windows][WG_VS]
+  int2* const vq_s = reinterpret_cast<int2*>(smem + WG_A1);  // [24 windows][WG_VS]: (value bits, argmax)
   const int sp = blockIdx.x;
   const int r = blockIdx.y;
   const int count = cnt[r];
@@ -1090,7 +1093,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   fetch_img(j_begin);
   for (int j = j_begin; j < j_end; ++j) {
     for (int band = 0; band < 6; ++band) {
-      __syncthreads();  // previous band's readers (a1_s, vq_s, sel_s; and img_s by its staging) done
+      __syncthreads();  // previous band's readers (a1_s, vq_s; and img_s by its staging) done
       if (band == 0) {
 #pragma unroll
         for (int k = 0; k < IMG_PRE; ++k)
@@ -1105,8 +1108,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const uint32_t c = pcd[s];
         const float v = (c & 0x80) ? pdv[s] : 0.0f;
         gb += v;
-        vq_s[(e >> 6) * WG_VS + (e & 63)] = v;
-        sel_s[(e >> 6) * WG_SS + (e & 63)] = (uint8_t)(c & 3);
+        vq_s[(e >> 6) * WG_VS + (e & 63)] = int2{__float_as_int(v), (int)(c & 3)};
       }
       // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles of 32 over the block's waves
 #pragma unroll
@@ -1118,7 +1120,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) {
             const int pw = min(t * 32 + acc_row(reg, kh), 6 * A1 - 1);  // clamped rows rewrite row 155's value
-            a1_s[pw * WG_CS + m] = fmaxf(a[reg], 0.0f);
+            a1_s[pw * WG_CS + 2 * (m & 15) + (m >> 4)] = fmaxf(a[reg], 0.0f);
           }
         }
       }
@@ -1131,14 +1133,20 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const int tb = 4 * st + kq;
         const int wr = tb / PL, wc = tb % PL;
         // V: B^T d B of the tile's 4x4 conv1 patch (rows 2*wr .., columns 2*wc ..), channels tl, 16 + tl
-        const float* d0 = a1_s + ((2 * wr + ra) * A1 + 2 * wc) * WG_CS + tl;
-        const int drow = (rb - ra) * A1 * WG_CS;
+        const fvec2* d0 = reinterpret_cast<const fvec2*>(a1_s + ((2 * wr + ra) * A1 + 2 * wc) * WG_CS) + tl;
+        const int drow = (rb - ra) * A1 * (WG_CS / 2);
+        fvec2 pa[4], pb[4];  // rows ra, rb of the patch, columns c: (ci tl, ci 16 + tl)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          pa[c] = d0[c * (WG_CS / 2)];
+          pb[c] = d0[drow + c * (WG_CS / 2)];
+        }
         float va[2][4];
 #pragma unroll
         for (int ch = 0; ch < 2; ++ch) {
           float t[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * WG_CS + 16 * ch] + sb * d0[drow + c * WG_CS + 16 * ch];
+          for (int c = 0; c < 4; ++c) t[c] = sa * pa[c][ch] + sb * pb[c][ch];
           va[ch][0] = t[0] - t[2];
           va[ch][1] = t[1] + t[2];
           va[ch][2] = t[2] - t[1];
@@ -1148,8 +1156,9 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         float db[4][4];
 #pragma unroll
         for (int cg = 0; cg < 4; ++cg) {
-          const float v = vq_s[tb * WG_VS + 16 * cg + tl];
-          const int sl = sel_s[tb * WG_SS + 16 * cg + tl];
+          const int2 vs = vq_s[tb * WG_VS + 16 * cg + tl];
+          const float v = __int_as_float(vs.x);
+          const int sl = vs.y;
           const float vi = ((sl & 2) ? ai1 : ai0) * v;
           const bool dx = (sl & 1) != 0;
           db[cg][0] = dx ? 0.0f : vi;
