@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/profile_$1
 rm -rf $O; mkdir -p $O
-K='conv_bwd_data_kernel|shapley_block_kernel'
+K='conv_bwd_data_kernel|conv_fwd_kernel|conv_wgrad_kernel|dense1_bwd_adam_kernel|dense_fwd_kernel|shapley_block_kernel'
 CMD="python bench.py --steps 1 --warmup 1 --no-cpu-baseline"
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $CMD > $O/trace.json 2> $O/trace.err && \
 timeout -k 10 500 rocprofv3 --kernel-include-regex "$K" --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- $CMD > $O/fetch.json 2> $O/fetch.err && \

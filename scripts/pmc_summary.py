@@ -18,8 +18,13 @@ for k, v in tot.items():
     # MFMA pipe utilisation: busy cycles over all 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE sums the
     # 8 XCDs, MI355X_MICROARCH.md)
     busy = v["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, v["GRBM_GUI_ACTIVE"] / 8 * 1024)
-    print(f"{k[:44]:44s} {busy:9.3f} {v['SQ_INSTS_VALU'] / mf:9.2f} {v['SQ_LDS_BANK_CONFLICT'] / (v['SQ_LDS_IDX_ACTIVE'] + 1):8.3f} "
-          f"{v['SQ_WAIT_INST_ANY'] / (v['SQ_ACTIVE_INST_ANY'] + 1):8.2f} {v['SQ_INSTS_VMEM_RD'] / mf:9.2f} "
+    if v["SQ_INSTS_MFMA"] > 0:
+        per = f"{v['SQ_INSTS_VALU'] / mf:9.2f}"
+        vm = f"{v['SQ_INSTS_VMEM_RD'] / mf:9.2f}"
+    else:  # no matrix instructions (HBM-bound kernels): ratios per MFMA are undefined
+        per, vm = f"{'-':>9s}", f"{'-':>9s}"
+    print(f"{k[:44]:44s} {busy:9.3f} {per} {v['SQ_LDS_BANK_CONFLICT'] / (v['SQ_LDS_IDX_ACTIVE'] + 1):8.3f} "
+          f"{v['SQ_WAIT_INST_ANY'] / (v['SQ_ACTIVE_INST_ANY'] + 1):8.2f} {vm} "
           f"{2 * v['FETCH_SIZE'] / 1024 / 1024:9.2f}")
 
 # extra view: where the waves spend their cycles (SQ_WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY)
@@ -28,4 +33,5 @@ for k, v in tot.items():
     wc = v["SQ_WAVE_CYCLES"] + 1e-9
     mf = v["SQ_INSTS_MFMA"] + 1e-9
     print(f"{k[:44]:44s} {v['SQ_WAVES']:8.0f} {v['SQ_WAIT_ANY'] / wc:8.3f} {v['SQ_WAIT_INST_ANY'] / wc:8.3f} "
-          f"{v['SQ_ACTIVE_INST_ANY'] / wc:8.3f} {v['SQ_INSTS_LDS'] / mf:8.2f} {v['SQ_WAIT_INST_LDS'] / wc:8.3f}")
+          f"{v['SQ_ACTIVE_INST_ANY'] / wc:8.3f} {(v['SQ_INSTS_LDS'] / mf if v['SQ_INSTS_MFMA'] > 0 else float('nan')):8.2f} "
+          f"{v['SQ_WAIT_INST_LDS'] / wc:8.3f}")
