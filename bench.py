@@ -94,10 +94,17 @@ def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # one rank per GPU; more ranks than GPUs (a gloo rehearsal of the multi-rank path on a 1-GPU box)
+    # share them round-robin
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    backend = os.environ.get("MPLC_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo for rehearsals
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, local
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, dev
 
 
 def barrier(world):
