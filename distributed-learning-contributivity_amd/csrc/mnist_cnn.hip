@@ -42,6 +42,7 @@ constexpr int NCLS = 10;
 constexpr int64_t OFF_W1 = MPLC_CNN_OFF_W1, OFF_B1 = MPLC_CNN_OFF_B1, OFF_W2 = MPLC_CNN_OFF_W2,
                   OFF_B2 = MPLC_CNN_OFF_B2, OFF_W3 = MPLC_CNN_OFF_W3, OFF_B3 = MPLC_CNN_OFF_B3,
                   OFF_W4 = MPLC_CNN_OFF_W4, OFF_B4 = MPLC_CNN_OFF_B4;
+constexpr int ADAM_LAST = 1 << 30;  // adam_t flag: the optimizer's last step
 constexpr int A1P = 33;  // padded channel stride of conv1 output tiles in LDS (bank-conflict-free A reads)
 
 // Cross-lane add within rows of 16 lanes on DPP (VALU, no LDS round trip).  Each level adds the partner's
@@ -159,7 +160,10 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
   idx[gid] = row;
   if (j == 0) {
     cnt[r] = c;
-    adam_t[r] = at;
+    // the optimizer's last step: its next step is idle or starts a fresh optimizer (slot index bmax: no row
+    // lookup, only the step's count and Adam iteration)
+    const SlotSched nx = schedule_slot(reps[r], bmax, step + 1, M, round_len, epochs, rows, splits, seq);
+    adam_t[r] = at | ((at > 0 && nx.at != at + 1) ? ADAM_LAST : 0);
   }
 }
 
@@ -451,27 +455,42 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------------
 // Keras 2.3.1 Adam (fresh state when t == 1: FedAvg builds a new optimizer per partner fit)
 // ------------------------------------------------------------------------------------------------
+// adam_t[r] = the replica's Adam iteration t (1-based; 0 = idle) | ADAM_LAST on the optimizer's last step
 struct AdamCfg {
   float lr_t, b1, b2, eps;
-  bool reset;
+  int t;
+  bool reset, last;
 };
 
-__device__ __forceinline__ AdamCfg adam_cfg(int t, float lr, float b1, float b2, float eps) {
+__device__ __forceinline__ AdamCfg adam_cfg(int t_flags, float lr, float b1, float b2, float eps) {
   AdamCfg c;
-  const float tf = (float)t;
+  c.t = t_flags & ~ADAM_LAST;
+  const float tf = (float)c.t;
   c.lr_t = lr * (sqrtf(1.0f - powf(b2, tf)) / (1.0f - powf(b1, tf)));
   c.b1 = b1;
   c.b2 = b2;
   c.eps = eps;
-  c.reset = (t == 1);
+  c.reset = (c.t == 1);
+  c.last = (t_flags & ADAM_LAST) != 0;
   return c;
 }
 
+// The moments after a fresh optimizer's first step, m1 = (1 - b1) g and v1 = (1 - b2) g^2, are functions of
+// that step's gradient alone: dense1_bwd_adam stores g there and rebuilds m1, v1 from it at step 2 with
+// this same routine (bit-identical), which halves the moment traffic of those two steps.
+__device__ __forceinline__ void adam_first_moments(float g, const AdamCfg& c, float& m1, float& v1) {
+  m1 = __fmul_rn(1.0f - c.b1, g);
+  v1 = __fmul_rn(1.0f - c.b2, __fmul_rn(g, g));
+}
+
 __device__ __forceinline__ void adam_apply(float& p, float& m, float& v, float g, const AdamCfg& c) {
-  const float m0 = c.reset ? 0.0f : m;
-  const float v0 = c.reset ? 0.0f : v;
-  const float mt = c.b1 * m0 + (1.0f - c.b1) * g;
-  const float vt = c.b2 * v0 + (1.0f - c.b2) * (g * g);
+  float mt, vt;
+  if (c.reset) {
+    adam_first_moments(g, c, mt, vt);
+  } else {
+    mt = c.b1 * m + (1.0f - c.b1) * g;
+    vt = c.b2 * v + (1.0f - c.b2) * (g * g);
+  }
   p = p - c.lr_t * mt / (sqrtf(vt) + c.eps);
   m = mt;
   v = vt;
@@ -618,7 +637,10 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   // access instruction covers 128 contiguous bytes per row, each dh_s read 8 adjacent 16-B slots
   const int c8 = tid & 7;
   const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
-  const bool fresh = cfg.reset;  // a fresh optimizer (first step of a round) never reads its moments
+  // W3's moments: a fresh optimizer's first step (t = 1) reads none and stores its gradient g1 in the m slot
+  // (not m1 and v1); step 2 reads g1 back and rebuilds m1, v1 (adam_first_moments); from step 3 on m and v
+  // are read and written as usual; an optimizer's last step writes neither (the next step starts fresh)
+  const bool fresh = cfg.reset, second = (cfg.t == 2);
   const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID;
   fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c8;
   fvec4* Mr = reinterpret_cast<fvec4*>(adam_m + roff) + c8;
@@ -633,7 +655,10 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     mv[i] = z4;
     vv[i] = z4;
   }
-  if (!fresh) {
+  if (second) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mv[i] = __builtin_nontemporal_load(Mr + 8 * i);  // g1
+  } else if (!fresh) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       mv[i] = __builtin_nontemporal_load(Mr + 8 * i);
@@ -691,14 +716,21 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float p1 = pw[q], m1 = mv[i][q], v1 = vv[i][q];
+      if (second) adam_first_moments(mv[i][q], cfg, m1, v1);
       adam_apply(p1, m1, v1, g[i][q], cfg);
       pw[q] = p1;
       mv[i][q] = m1;
       vv[i][q] = v1;
     }
     W[8 * i] = pw;
-    __builtin_nontemporal_store(mv[i], Mr + 8 * i);
-    __builtin_nontemporal_store(vv[i], Vr + 8 * i);
+    if (!cfg.last) {
+      if (fresh) {
+        __builtin_nontemporal_store(g[i], Mr + 8 * i);
+      } else {
+        __builtin_nontemporal_store(mv[i], Mr + 8 * i);
+        __builtin_nontemporal_store(vv[i], Vr + 8 * i);
+      }
+    }
   }
   if (k0 == 0 && tid < HID) {  // the replica's slice-0 block (logical order)
     float gb = 0.0f;

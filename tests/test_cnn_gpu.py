@@ -74,6 +74,10 @@ def test_schedule_bit_exact(scenario, engine):
             expect = steps[t] if t < len(steps) else np.array([], dtype=np.int64)
             assert cnt[r] == len(expect)
             assert idx[r, :cnt[r]].tolist() == [int(v) for v in expect]
+            at = st.ws["adam_t"].cpu().numpy()
+            last = 1 << 30  # the optimizer's last step (no moments stored): the round's final step
+            assert (at[r] & ~last) == (t + 1 if t < len(steps) else 0)
+            assert bool(at[r] & last) == (t == len(steps) - 1)
         spe = -(-len(prow[2]) // bs[2])
         es_, ts = divmod(s, spe)
         srows = ocnn.single_epoch_rows(ocnn.shuffle_key(engine.seed, 0b100, 2), prow[2], bs[2], es_)[ts]
@@ -81,7 +85,9 @@ def test_schedule_bit_exact(scenario, engine):
 
 
 def test_one_step_gradients_and_activations(scenario, engine, odata):
-    """lr = 0: Adam's first moment after step 1 is (1 - beta1) * g, which exposes the device gradient."""
+    """lr = 0: Adam's first moment after step 1 is (1 - beta1) * g, which exposes the device gradient.  W3's
+    slot holds g itself (dense1_bwd_adam stores a fresh optimizer's first gradient and rebuilds m1, v1 from
+    it at step 2)."""
     import torch
     coal = [(0, 1), (1, 2)]
     st = engine.trainer.prepare(coal, 1)
@@ -107,7 +113,7 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
         g_dev = m[r] / np.float32(0.1)
         for name, (off, shape) in ocnn.OFF.items():
             n = int(np.prod(shape))
-            gd = g_dev[off:off + n].astype(np.float64)
+            gd = (m[r] if name == "W3" else g_dev)[off:off + n].astype(np.float64)
             ref = g64[name].numpy().reshape(-1)
             scale = max(np.linalg.norm(ref), 1e-12)
             err_dev = np.linalg.norm(gd - ref) / scale

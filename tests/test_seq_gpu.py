@@ -57,7 +57,11 @@ def test_sequential_schedule_bit_exact():
                 idx = st.ws["idx"].cpu().numpy()
                 at = st.ws["adam_t"].cpu().numpy()
                 if t < len(expect):
-                    assert cnt[0] == len(expect[t]) and at[0] == t + 1
+                    # Adam iteration, plus the last-step flag (bit 30) on the round's final step: the next
+                    # step starts a fresh optimizer, so the step stores no moments
+                    last = 1 << 30
+                    assert cnt[0] == len(expect[t]) and (at[0] & ~last) == t + 1
+                    assert bool(at[0] & last) == (t == len(expect) - 1)
                     assert idx[0, :cnt[0]].tolist() == [int(v) for v in expect[t]]
                 else:
                     assert cnt[0] == 0
