@@ -52,6 +52,49 @@ CONV_BWD_DATA_FLOP_PER_SAMPLE = 169 * 16 * 64 * 32 * 2
 CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE = 676 * 32 * 576 * 2
 MNIST_FWD_FLOP = 23984896       # per sample, SURVEY A21
 MNIST_TRAIN_FLOP = 71565312     # per sample (fwd + wgrad + dgrad, no conv1 dgrad)
+# The training step's kernels (csrc/mnist_cnn.hip, timed in stream with HIP events) and the algorithmic unit of
+# each: (bound, unit of the rate, units per sample or the stash key, description).  The convolutions are priced at
+# the Winograd F(2x2,3x3) algorithm's own conv2 multiply-adds (what the matrix cores execute); the W3 kernels at
+# the HBM bytes their access pattern must move.
+WINO_FWD_FLOP_PER_SAMPLE = 144 * 16 * 32 * 64 * 2  # 144 pool-window tiles x 16 points x 32 ci x 64 co
+KERNEL_UNITS = {
+    "conv_fwd": ("mfma", "TFLOP/s", WINO_FWD_FLOP_PER_SAMPLE,
+                 "conv2's Winograd multiply-adds, 144 tiles x 16 points x 32 x 64 per sample"),
+    "dense_fwd": ("hbm", "GB/s", "dense_fwd_bytes", "W3 read + the pooled row read and hidden row written per sample"),
+    "head": (None, None, None, "Dense(10) + softmax-CE + Adam(W4): one block per replica, latency-bound"),
+    "dense1_bwd_adam": ("hbm", "GB/s", "dense1_bwd_adam_bytes",
+                        "W3 read and written, Adam moments read/written by optimizer step, pooled + dh read and "
+                        "dpooled written per sample"),
+    "conv_bwd_data": ("mfma", "TFLOP/s", CONV_BWD_DATA_FLOP_PER_SAMPLE,
+                      "the data gradient's Winograd multiply-adds, 169 tiles x 16 points x 64 x 32 per sample"),
+    "conv_wgrad": ("mfma", "TFLOP/s", WINO_FWD_FLOP_PER_SAMPLE,
+                   "dW2's Winograd F(3x3,2x2) multiply-adds, 144 tiles x 16 points x 32 x 64 per sample"),
+    "adam_small": (None, None, None, "Adam on W1/b1/W2/b2 from the per-sample partials"),
+}
+TRAIN_KERNELS = list(KERNEL_UNITS)
+
+
+def kernel_table(timer, units):
+    """Per training kernel: launches, in-stream ms (HIP events on the launch stream), share of the step's kernel
+    time and, for the kernels with an algorithmic unit, the achieved rate against its roofline."""
+    tot = sum(timer.total_ms(k) for k in TRAIN_KERNELS) or 1.0
+    out = {}
+    for k, (bound, unit, per, desc) in KERNEL_UNITS.items():
+        ms, n = timer.total_ms(k), timer.launches(k)
+        e = {"launches": n, "ms_total": round(ms, 1), "ms_avg": round(ms / max(1, n), 4),
+             "time_share": round(ms / tot, 4)}
+        if bound is not None and ms > 0 and units:
+            amount = units[per] if isinstance(per, str) else units["samples"] * per
+            if bound == "hbm":
+                rate, peak = amount / (ms / 1000) / 1e9, HBM_PEAK_GBS
+            else:
+                rate, peak = amount / (ms / 1000) / 1e12, FP32_MFMA_PEAK_TFLOPS
+            e.update({"bound": bound, "achieved": round(rate, 2), "peak": peak, "unit": unit,
+                      "frac": round(rate / peak, 4), "units_per_launch": int(amount / max(1, n)), "algorithmic": desc})
+        out[k] = e
+    return out
+
+
 TRAFFIC_SOURCE = ("profiles/pmc_traffic.json: FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes of "
                   "this same command (scripts/pmc_traffic.py), not measured in this run")
 
@@ -383,12 +426,12 @@ def bench_train(args, rank, world):
         c.compute_contributivity("Shapley values")
         return c
 
-    timer = KernelTimer(args.profile_kernel)
-    reps0 = [0]
+    timer = KernelTimer("all", TRAIN_KERNELS, stash=True)
+    reps0 = [None]
 
     def timed_step():
-        if eng.profiler is None:  # the timed region starts: attach the in-stream kernel timer
-            eng.profiler = timer
+        if eng.profiler is None and reps0[0] is None:  # the timed region starts: attach the in-stream timer
+            eng.profiler = None if args.no_kernel_timer else timer
             reps0[0] = eng.stats["replicas"]
         return one_step()
 
@@ -396,21 +439,34 @@ def bench_train(args, rank, world):
     reserve = (0 if args.no_shapley_agg else 15) + (45 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
     steps, warm, wall, c = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
-    kern_ms = timer.total_ms()
-    launches = timer.launches()
+    units = eng.model_impl.algorithmic_units(timer.stash)
+    timer.stash = []
+    kernels = kernel_table(timer, units)
     local_reps = eng.stats["replicas"] - reps0[0]
-    sizes = eng.partner_sizes
-    # exact per-rank sample count: sum over this rank's replicas of E * n_p (shard is LPT over coalitions)
-    from mplc.parallel import lpt_shard, coalition_cost
-    from itertools import combinations
-    coals = [cc for r in range(1, n + 1) for cc in combinations(range(n), r)]
-    shards = lpt_shard([coalition_cost(cc, sizes) for cc in coals], world)
-    mine = [coals[i] for i in shards[rank]]
-    samples = steps * args.epochs * sum(sizes[p] for cc in mine for p in cc)
-    flops = samples * CONV_BWD_DATA_FLOP_PER_SAMPLE
-    achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
+    samples = units.get("samples", 0.0)
     ms_per_step = wall * 1000 / steps
     total_train_samples = sum_over_ranks(samples, world)
+    # the roofline kernel: the one with the largest share of the step's kernel time
+    if args.no_kernel_timer:  # counter-collection passes (scripts/gpu_profile.sh): no events in the stream
+        kernels = {}
+        samples = steps * args.epochs * sum(eng.partner_sizes) * (2 ** (n - 1)) / world
+        total_train_samples = sum_over_ranks(samples, world)
+    dom = max((k for k in kernels if "frac" in kernels[k]), key=lambda k: kernels[k]["ms_total"], default=None)
+    kd = kernels.get(dom, {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                           "launches": 0, "ms_avg": None, "time_share": None, "units_per_launch": None})
+    roof = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
+            "frac": kd["frac"], "traffic": None, "kernel": f"{dom}_kernel", "launches": kd["launches"],
+            "kernel_ms_avg": kd["ms_avg"], "time_share": kd["time_share"]}
+    if dom is None:
+        roof["note"] = "in-stream kernel timing off (--no-kernel-timer)"
+    elif kd["bound"] == "hbm":
+        roof["algorithmic_bytes_per_launch"] = kd["units_per_launch"]
+        roof["note"] = ("the step's dominant kernel; achieved = its algorithmic HBM bytes (" + KERNEL_UNITS[dom][3] +
+                        ", counted per launch from the step's own schedule) / in-stream kernel time (HIP events "
+                        "on the launch stream)")
+    else:
+        roof["algorithmic_flop_per_launch"] = kd["units_per_launch"]
+        roof["note"] = ("the step's dominant kernel; achieved = " + KERNEL_UNITS[dom][3] + " / in-stream kernel time")
     out = {
         "metric": "coalition v(S) evals/sec (MNIST FedAvg)",
         "value": round(n_coal * steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
@@ -428,19 +484,8 @@ def bench_train(args, rank, world):
         "budget": {"budget_s": args.budget_s, "steps_requested": args.steps, "warmup_requested": args.warmup,
                    "timed_wall_s": round(wall, 2), "note": "one step = one whole 1023-coalition sweep; K clamped to "
                                                           "the whole steps that fit the wall-clock budget"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": f"{args.profile_kernel}_kernel", "launches": launches,
-                     "kernel_ms_avg": round(kern_ms / max(1, launches), 4),
-                     "algorithmic_flop_per_launch": int(flops / max(1, launches)),
-                     "flop_per_sample": CONV_BWD_DATA_FLOP_PER_SAMPLE,
-                     "direct_conv_flop_per_sample": CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE,
-                     "direct_conv_equivalent_tflops": round(achieved * CONV_BWD_DATA_DIRECT_FLOP_PER_SAMPLE
-                                                            / CONV_BWD_DATA_FLOP_PER_SAMPLE, 2),
-                     "note": "achieved = the Winograd F(2x2,3x3) algorithm's own fp32 multiply-adds (169 tiles x "
-                             "16 points x 64 x 32 per sample) / in-stream kernel time, i.e. how busy the matrix "
-                             "cores are; the direct convolution the reference computes is 2.25x more FLOPs "
-                             "(direct_conv_equivalent_tflops)"},
+        "roofline": roof,
+        "kernels": kernels,
         "shapley_values": [round(float(v), 6) for v in c.contributivity_scores],
         # coalition evaluations as the reference counts them, and the realised epochs (fixed E,
         # early stopping off, so every coalition trains exactly E epochs)
@@ -580,9 +625,10 @@ def main():
     ap.add_argument("--minibatches", type=int, default=20)
     ap.add_argument("--gupp", type=int, default=8)
     ap.add_argument("--n", type=int, default=28)
-    ap.add_argument("--profile-kernel", default="conv_bwd_data")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shapley-agg", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true",
+                    help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()
     rank, world, _ = dist_init()
     if args.leg == "shapley":
@@ -601,7 +647,10 @@ def main():
     else:
         out, sc = bench_train(args, rank, world)
         wl = out["config"]["workload"]
-        out["roofline"]["traffic"] = pmc_traffic(f"{args.profile_kernel}_kernel", wl)
+        out["roofline"]["traffic"] = pmc_traffic(out["roofline"]["kernel"], wl)
+        for k, e in out["kernels"].items():  # PMC bytes per launch beside each kernel's algorithmic count
+            if e.get("bound") == "hbm":
+                e["traffic_pmc"] = pmc_traffic(f"{k}_kernel", wl)
         out["roofline"]["traffic_source"] = TRAFFIC_SOURCE
         if not args.no_shapley_agg:
             # the lockstep training batch's buffers are no longer needed: give the 2 GiB table room

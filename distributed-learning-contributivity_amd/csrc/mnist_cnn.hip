@@ -1345,10 +1345,17 @@ int mplc_cnn_copy_rows(float* dst, const float* src, int64_t stride, const int32
   return launch_status();
 }
 
-#define PROF_BEGIN(k) \
-  if (t->prof_kernel == (k) && t->prof_begin) (void)hipEventRecord((hipEvent_t)t->prof_begin, s)
-#define PROF_END(k) \
-  if (t->prof_kernel == (k) && t->prof_end) (void)hipEventRecord((hipEvent_t)t->prof_end, s)
+// In-stream kernel timing (bench.py): prof_kernel = k > 0 records the events prof_begin / prof_end around
+// launch k; prof_kernel = MPLC_PROF_ALL records around every launch k, with prof_begin / prof_end then pointing
+// to arrays of hipEvent_t indexed by k (1 .. MPLC_PROF_KERNELS).
+static inline void prof_record(const mplc_cnn_train_t* t, int k, bool end, hipStream_t s) {
+  void* ev = end ? t->prof_end : t->prof_begin;
+  if (!ev) return;
+  if (t->prof_kernel == k) (void)hipEventRecord((hipEvent_t)ev, s);
+  else if (t->prof_kernel == MPLC_PROF_ALL) (void)hipEventRecord(static_cast<hipEvent_t*>(ev)[k], s);
+}
+#define PROF_BEGIN(k) prof_record(t, (k), false, s)
+#define PROF_END(k) prof_record(t, (k), true, s)
 
 int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   if (!t || t->n_rep < 1 || t->n_rep > 65535 || t->bmax < 1) return MPLC_E_ARG;

@@ -29,6 +29,8 @@ W2P = 18496
 W1_BANDS = 3  # MPLC_CNN_W1_BANDS: [dW1 | db1] partials per sample (data-gradient blocks)
 W2T = 32768  # MPLC_CNN_W2T: W2 in Winograd form (forward), then transposed (data gradient)
 WG_SAMPLES = 8
+ADAM_LAST = 1 << 30  # adam_t flag (csrc/mnist_cnn.hip): the optimizer's last step
+PROF_ALL = -1        # mplc_cnn_train_t.prof_kernel (MPLC_PROF_ALL): time every launch of the step
 PATIENCE = 10
 
 # Keras get_weights() order of the MNIST model (mplc/dataset.py:460-471): (offset in a model row, shape)
@@ -221,10 +223,42 @@ class MnistModel:
     def step(self, st, s, prof):
         st.t.step = s
         if prof is not None:
+            if prof.all:
+                prof.bind(self.KERNEL_IDS)
             ev0, ev1 = prof.pair()
-            st.t.prof_kernel = self.KERNEL_IDS[prof.kernel]
+            st.t.prof_kernel = PROF_ALL if prof.all else self.KERNEL_IDS[prof.kernel]
             st.t.prof_begin, st.t.prof_end = ev0, ev1
+        else:
+            st.t.prof_kernel, st.t.prof_begin, st.t.prof_end = 0, None, None
         _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(st.t), st.stream), "mplc_cnn_train_step")
+        if prof is not None and prof.want_stash:
+            prof.stash_step(st.ws["cnt"], st.ws["adam_t"])
+
+    @staticmethod
+    def algorithmic_units(stash):
+        """Algorithmic work of the timed steps from their stashed schedules [(cnt, adam_t)], per kernel:
+        samples (the convolution kernels' unit) and the HBM bytes the two W3 kernels must move
+        (csrc/mnist_cnn.hip dense_fwd_kernel / dense1_bwd_adam_kernel):
+          dense_fwd:       W3 read + per sample its pooled row read and hidden row written;
+          dense1_bwd_adam: W3 read and written; Adam moments by the optimizer step t - t = 1 writes the
+                           gradient into the m slot, t = 2 reads it and writes m and v, t >= 3 reads and
+                           writes m and v, the optimizer's last step writes no moments; per sample the pooled
+                           row and dh read, the dpooled row written."""
+        import torch
+        if not stash:
+            return {}
+        cnt = torch.stack([c for c, _ in stash]).to(torch.float64)
+        at = torch.stack([a for _, a in stash])
+        t = at & (ADAM_LAST - 1)
+        last = (at & ADAM_LAST) != 0
+        act = (cnt > 0).to(torch.float64)
+        w3 = float(FEAT * HID * 4)
+        mom_rd = torch.where(t == 1, 0.0, torch.where(t == 2, 1.0, 2.0)).to(torch.float64)
+        mom_wr = torch.where(last, 0.0, torch.where(t == 1, 1.0, 2.0)).to(torch.float64)
+        d1 = act * (w3 * (2.0 + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
+        df = act * (w3 + cnt * float(FEAT * 4 + HID * 4))
+        return {"samples": float(cnt.sum().item()), "dense1_bwd_adam_bytes": float(d1.sum().item()),
+                "dense_fwd_bytes": float(df.sum().item())}
 
     def evaluate(self, eng, sel, x, y):
         """(correct counts, mean CE) of the C models in `sel` [C][STRIDE] on (x, y)."""

@@ -1,14 +1,35 @@
-"""In-stream kernel timing for the bench roofline: a pair of HIP events recorded around one chosen kernel of
-every training step (mplc_cnn_train_t.prof_kernel), on the stream the kernel is launched on."""
+"""In-stream kernel timing for the bench roofline: HIP events recorded by the library around the kernels of
+every training step (mplc_cnn_train_t.prof_kernel), on the stream the kernels are launched on.
+
+KernelTimer("conv_bwd_data") times one kernel; KernelTimer("all", names) times every launch of the step
+(prof_kernel = MPLC_PROF_ALL, the event handles passed as arrays indexed by kernel id).  Completed event pairs
+are folded into running totals with non-blocking queries, so a long timed region keeps only the last few
+steps' events alive and never synchronises.
+
+With stash=True the model also keeps a device copy of each step's schedule (cnt, adam_t), from which the
+algorithmic units of every kernel (samples; the dense kernels' HBM bytes, which depend on the Adam step) are
+counted exactly after the timed region (MnistModel.algorithmic_units)."""
+import ctypes
+
+PROF_ALL = -1  # include/mplc_hip_cnn.h MPLC_PROF_ALL
 
 
 class KernelTimer:
-    def __init__(self, kernel):
+    def __init__(self, kernel, names=None, stash=False):
         self.kernel = kernel
-        self.events = []
-        self.samples = []
+        self.want_stash = stash
+        self.names = list(names) if names is not None else [kernel]
+        self.pending = []            # [(name, begin, end)]
+        self.ms = {n: 0.0 for n in self.names}
+        self.count = {n: 0 for n in self.names}
+        self._keep = []              # ctypes arrays passed to the library for the pending steps
+        self.stash = []              # per step: device copies of the schedule tensors the model accounts from
 
-    def pair(self):
+    @property
+    def all(self):
+        return self.kernel == "all"
+
+    def _event_pair(self):
         import torch
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -16,13 +37,55 @@ class KernelTimer:
         # re-records both inside the step, in stream order, so elapsed_time covers exactly the kernel
         a.record()
         b.record()
-        self.events.append((a, b))
-        return a.cuda_event, b.cuda_event
+        return a, b
 
-    def total_ms(self):
+    def _fold(self, block=False):
+        keep = []
+        for name, a, b in self.pending:
+            if block or b.query():
+                self.ms[name] += a.elapsed_time(b)
+                self.count[name] += 1
+            else:
+                keep.append((name, a, b))
+        self.pending = keep
+        if len(self._keep) > 64:
+            self._keep = self._keep[-64:]
+
+    def pair(self):
+        """(begin, end) handles for one step: hipEvent_t values, or for "all" pointers to hipEvent_t arrays
+        indexed by kernel id (ids = the model's KERNEL_IDS)."""
+        if len(self.pending) > 256:
+            self._fold()
+        if not self.all:
+            a, b = self._event_pair()
+            self.pending.append((self.kernel, a, b))
+            return a.cuda_event, b.cuda_event
+        n = max(self.ids.values()) + 1
+        begin = (ctypes.c_void_p * n)()
+        end = (ctypes.c_void_p * n)()
+        for name, k in self.ids.items():
+            a, b = self._event_pair()
+            begin[k], end[k] = a.cuda_event, b.cuda_event
+            self.pending.append((name, a, b))
+        self._keep.append((begin, end))
+        return ctypes.addressof(begin), ctypes.addressof(end)
+
+    def bind(self, kernel_ids):
+        """Kernel ids of the model being timed (its KERNEL_IDS)."""
+        self.ids = {n: kernel_ids[n] for n in self.names}
+        return self
+
+    def stash_step(self, *tensors):
+        """Keep device copies of a step's schedule tensors (cnt, adam_t) for the algorithmic-unit count made
+        after the timed region (a copy per tensor and step: no host sync inside the region)."""
+        self.stash.append(tuple(t.clone() for t in tensors))
+
+    def total_ms(self, name=None):
         import torch
         torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in self.events)
+        self._fold(block=True)
+        return self.ms[name or self.kernel]
 
-    def launches(self):
-        return len(self.events)
+    def launches(self, name=None):
+        self._fold(block=True)
+        return self.count[name or self.kernel]

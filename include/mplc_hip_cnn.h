@@ -43,6 +43,8 @@ extern "C" {
 #define MPLC_CNN_OFF_B4 1199872    /* 10         */
 #define MPLC_CNN_NPARAM 1199882
 #define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
+#define MPLC_PROF_ALL (-1)         /* mplc_cnn_train_t.prof_kernel: time every launch of the step */
+#define MPLC_PROF_KERNELS 7
 #define MPLC_CNN_W1_BANDS 3        /* data-gradient blocks per sample (64 Winograd tiles each) */
 #define MPLC_CNN_W2T 32768         /* per-model W2 workspace: 16 Winograd planes x 32 x 64 floats */
 #define MPLC_CNN_FEAT 9216         /* flattened pooled features */
@@ -113,7 +115,9 @@ typedef struct {
   float lr, beta1, beta2, eps;
   /* optional in-stream timing of one kernel of the step (bench roofline): hipEvent_t recorded right
    * before / after launch number prof_kernel (1 conv_fwd, 2 dense_fwd, 3 head, 4 dense1_bwd_adam,
-   * 5 conv_bwd_data, 6 conv_wgrad, 7 adam_small); 0 or NULL events = off */
+   * 5 conv_bwd_data, 6 conv_wgrad, 7 adam_small); 0 or NULL events = off.  prof_kernel = MPLC_PROF_ALL (-1):
+   * every launch k is timed, prof_begin / prof_end then point to hipEvent_t arrays of MPLC_PROF_KERNELS + 1
+   * entries indexed by k */
   int32_t prof_kernel;
   int32_t pad1;
   void* prof_begin;

@@ -1,0 +1,54 @@
+"""Host-side accounting of the bench's per-kernel rates (bench.py kernel_table, MnistModel.algorithmic_units):
+the dense kernels' algorithmic HBM bytes follow the Adam schedule flags exactly as csrc/mnist_cnn.hip
+dense1_bwd_adam_kernel moves them.  No GPU needed."""
+import os
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "distributed-learning-contributivity_amd"))
+
+from mplc import cnn  # noqa: E402
+
+W3 = 9216 * 128 * 4
+
+
+def test_dense_bytes_follow_adam_schedule():
+    L = cnn.ADAM_LAST
+    # replicas: fresh step (t=1), idle, step 2, step 5, last step of an optimizer (t=8), t=1 that is also last
+    cnt = torch.tensor([27, 0, 27, 10, 27, 5], dtype=torch.int32)
+    at = torch.tensor([1, 0, 2, 5, 8 | L, 1 | L], dtype=torch.int32)
+    u = cnn.MnistModel.algorithmic_units([(cnt, at)])
+    per_sample_bwd = 2 * 9216 * 4 + 128 * 4
+    # W3 read+write (2) + moments: t1 -> write g (1); t2 -> read g, write m, v (3); t5 -> 4; last t8 -> read 2;
+    # t1 last -> nothing
+    moments = [1, None, 3, 4, 2, 0]
+    exp = sum((2 + m) * W3 + c * per_sample_bwd for c, m in zip([27, 0, 27, 10, 27, 5], moments) if m is not None)
+    assert u["dense1_bwd_adam_bytes"] == exp
+    assert u["dense_fwd_bytes"] == 5 * W3 + 96 * (9216 * 4 + 128 * 4)
+    assert u["samples"] == 96
+
+
+def test_kernel_table_picks_rates():
+    import bench
+
+    class FakeTimer:
+        def total_ms(self, k):
+            return {"dense1_bwd_adam": 20.0, "conv_bwd_data": 10.0}.get(k, 1.0)
+
+        def launches(self, k):
+            return 2
+
+    units = {"samples": 1000.0, "dense1_bwd_adam_bytes": 1.2e11, "dense_fwd_bytes": 3e10}
+    tab = bench.kernel_table(FakeTimer(), units)
+    d1 = tab["dense1_bwd_adam"]
+    assert d1["bound"] == "hbm" and d1["achieved"] == pytest.approx(1.2e11 / 0.02 / 1e9)
+    assert d1["frac"] == pytest.approx(d1["achieved"] / 8000.0, abs=1e-4)
+    cb = tab["conv_bwd_data"]
+    assert cb["achieved"] == pytest.approx(1000 * bench.CONV_BWD_DATA_FLOP_PER_SAMPLE / 0.01 / 1e12, abs=0.01)
+    assert "frac" not in tab["head"]
+    assert sum(e["time_share"] for e in tab.values()) == pytest.approx(1.0, abs=1e-3)
