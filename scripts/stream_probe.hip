@@ -2,7 +2,8 @@
 // arithmetic: per 32-row x 128-col slice of every replica's W3, read W, m, v and write them back (the
 // Adam pass), with the same block shape, fvec4 layout and nontemporal moments as the kernel.
 // Variants: rmw3 (the pattern), rmw3_plain (no nontemporal hints), read3 (reads only), copy1 (one stream
-// read, one written).  Build: hipcc -O3 --offload-arch=gfx950 scripts/stream_probe.hip -o stream_probe
+// read, one written), rmw3_allnt (W nontemporal too), rmw3_pipe<S> (S slices per block, the next slice's loads
+// in flight during the current slice's stores).  Build: hipcc -O3 --offload-arch=gfx950 scripts/stream_probe.hip -o stream_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -35,6 +36,65 @@ __global__ __launch_bounds__(256) void rmw3(float* P, float* M, float* V) {
       Mr[8 * i] = m[i] * 0.9f;
       Vr[8 * i] = v[i] * 0.99f;
     }
+  }
+}
+
+// every access nontemporal (W too)
+__global__ __launch_bounds__(256) void rmw3_allnt(float* P, float* M, float* V) {
+  const int r = blockIdx.y, k0 = blockIdx.x * ROWS, tid = threadIdx.x, rowl = tid >> 3, c8 = tid & 7;
+  const int64_t off = (int64_t)r * STRIDE + OFF_W3 + (int64_t)(k0 + rowl) * HID;
+  fvec4* W = reinterpret_cast<fvec4*>(P + off) + c8;
+  fvec4* Mr = reinterpret_cast<fvec4*>(M + off) + c8;
+  fvec4* Vr = reinterpret_cast<fvec4*>(V + off) + c8;
+  fvec4 w[4], m[4], v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = __builtin_nontemporal_load(W + 8 * i);
+    m[i] = __builtin_nontemporal_load(Mr + 8 * i);
+    v[i] = __builtin_nontemporal_load(Vr + 8 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    __builtin_nontemporal_store(w[i] + 1e-7f, W + 8 * i);
+    __builtin_nontemporal_store(m[i] * 0.9f, Mr + 8 * i);
+    __builtin_nontemporal_store(v[i] * 0.99f, Vr + 8 * i);
+  }
+}
+
+// S consecutive slices per block, the loads of slice s+1 issued before the stores of slice s
+template <int S>
+__global__ __launch_bounds__(256) void rmw3_pipe(float* P, float* M, float* V) {
+  const int r = blockIdx.y, tid = threadIdx.x, rowl = tid >> 3, c8 = tid & 7;
+  fvec4 w[2][4], m[2][4], v[2][4];
+  auto ld = [&](int s, int b) {
+    const int64_t off = (int64_t)r * STRIDE + OFF_W3 + (int64_t)((blockIdx.x * S + s) * ROWS + rowl) * HID;
+    fvec4* W = reinterpret_cast<fvec4*>(P + off) + c8;
+    fvec4* Mr = reinterpret_cast<fvec4*>(M + off) + c8;
+    fvec4* Vr = reinterpret_cast<fvec4*>(V + off) + c8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[b][i] = W[8 * i];
+      m[b][i] = __builtin_nontemporal_load(Mr + 8 * i);
+      v[b][i] = __builtin_nontemporal_load(Vr + 8 * i);
+    }
+  };
+  auto st = [&](int s, int b) {
+    const int64_t off = (int64_t)r * STRIDE + OFF_W3 + (int64_t)((blockIdx.x * S + s) * ROWS + rowl) * HID;
+    fvec4* W = reinterpret_cast<fvec4*>(P + off) + c8;
+    fvec4* Mr = reinterpret_cast<fvec4*>(M + off) + c8;
+    fvec4* Vr = reinterpret_cast<fvec4*>(V + off) + c8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      W[8 * i] = w[b][i] + 1e-7f;
+      __builtin_nontemporal_store(m[b][i] * 0.9f, Mr + 8 * i);
+      __builtin_nontemporal_store(v[b][i] * 0.99f, Vr + 8 * i);
+    }
+  };
+  ld(0, 0);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) ld(s + 1, (s + 1) & 1);
+    st(s, s & 1);
   }
 }
 
@@ -81,7 +141,8 @@ int main(int argc, char** argv) {
   const dim3 grid(FEAT / ROWS, R);
   const double slice = (double)R * FEAT * HID * 4;  // bytes of one stream
   const int reps = 10;
-  for (int variant = 0; variant < 4; ++variant) {
+  const char* names[] = {"rmw3_nt", "rmw3_plain", "read3", "copy1", "rmw3_allnt", "rmw3_pipe2", "rmw3_pipe4"};
+  for (int variant = 0; variant < 7; ++variant) {
     for (int rep = 0; rep < 2; ++rep) {  // first pass warms
       CK(hipEventRecord(a));
       for (int i = 0; i < reps; ++i) {
@@ -89,15 +150,18 @@ int main(int argc, char** argv) {
         if (variant == 1) rmw3<false><<<grid, 256>>>(P, M, V);
         if (variant == 2) read3<<<grid, 256>>>(P, M, V, out);
         if (variant == 3) copy1<<<grid, 256>>>(P, M);
+        if (variant == 4) rmw3_allnt<<<grid, 256>>>(P, M, V);
+        if (variant == 5) rmw3_pipe<2><<<dim3(FEAT / ROWS / 2, R), 256>>>(P, M, V);
+        if (variant == 6) rmw3_pipe<4><<<dim3(FEAT / ROWS / 4, R), 256>>>(P, M, V);
       }
       CK(hipEventRecord(b));
       CK(hipEventSynchronize(b));
       float ms;
       CK(hipEventElapsedTime(&ms, a, b));
-      const double bytes = slice * (variant <= 1 ? 6 : variant == 2 ? 3 : 2);
+      const double bytes = slice * (variant == 2 ? 3 : variant == 3 ? 2 : 6);
       if (rep == 1)
         printf("%-12s R=%d  %.3f ms/launch  %.2f TB/s\n",
-               variant == 0 ? "rmw3_nt" : variant == 1 ? "rmw3_plain" : variant == 2 ? "read3" : "copy1", R,
+               names[variant], R,
                ms / reps, bytes / (ms / reps * 1e-3) / 1e12);
     }
   }
