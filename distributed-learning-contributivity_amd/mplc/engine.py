@@ -92,7 +92,7 @@ class CoalitionEngine:
             memory_budget_bytes = max(int(free * 0.8) - self.eval_budget_bytes, 1 << 30)
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
-        self.profiler = None  # optional KernelTimer (bench.py): HIP events around one kernel per step
+        self.profiler = None  # optional KernelTimer (bench.py): in-stream HIP events around the step kernels
         self.stats = {"coalitions": 0, "batches": 0, "replicas": 0, "samples": 0}
 
     # --------------------------------------------------------------------------------------------

@@ -188,6 +188,30 @@ def test_values_independent_of_batch_composition(engine):
     assert together[5] == alone[0] and together[2] == alone[1]
 
 
+def test_all_kernel_timer_is_result_neutral(engine):
+    """bench.py's in-stream timing of every launch (prof_kernel = MPLC_PROF_ALL, event arrays) neither
+    changes v(S) nor misses a launch, and the stashed schedules count every trained sample."""
+    from mplc.cnn import KERNEL_IDS
+    from mplc.profiling import KernelTimer
+    all7 = [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
+    timer = KernelTimer("all", list(KERNEL_IDS), stash=True)
+    engine.profiler = timer
+    try:
+        timed = engine.evaluate(all7)
+    finally:
+        engine.profiler = None
+    plain = engine.evaluate(all7)
+    assert np.array_equal(timed, plain)
+    steps = len(timer.stash)
+    assert steps > 0
+    for k in KERNEL_IDS:
+        assert timer.launches(k) == steps and timer.total_ms(k) > 0.0
+    units = engine.model_impl.algorithmic_units(timer.stash)
+    sizes = engine.partner_sizes
+    assert units["samples"] == engine.epoch_count * sum(sizes[p] for c in all7 for p in c)
+    assert units["dense1_bwd_adam_bytes"] > units["dense_fwd_bytes"] > 0
+
+
 def test_coalition_accuracies_vs_oracle(scenario, engine, odata):
     prow, bs = rows(scenario)
     all7 = [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
