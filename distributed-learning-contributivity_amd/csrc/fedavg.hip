@@ -9,7 +9,7 @@
 // exactly that per element (fp-contract off: no FMA), so the fp32 result is bit-identical.
 //
 // Roofline: HBM-bound. Algorithmic bytes per coalition = 4 * n_param * (|S| read + 1 write
-// [+ |S| broadcast writes]).
+// [+ |S| broadcast writes, minus the skipped range of mplc_fedavg_aggregate_bcast_skip]).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "mplc_hip.h"
@@ -24,7 +24,7 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
                                                      const int32_t* __restrict__ first, const double* __restrict__ w,
                                                      const double* __restrict__ scale, int64_t n_param,
                                                      float* __restrict__ out, int64_t out_stride, int broadcast,
-                                                     int vec4) {
+                                                     int64_t skip_lo, int64_t skip_hi, int vec4) {
   const int c = blockIdx.y;
   const int r0 = first[c];
   const int r1 = first[c + 1];
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
       }
       const float4 res = make_float4((float)(s0 / scl), (float)(s1 / scl), (float)(s2 / scl), (float)(s3 / scl));
       if (out) reinterpret_cast<float4*>(out + (int64_t)c * out_stride)[k] = res;
-      if (broadcast)
+      if (broadcast && (4 * k < skip_lo || 4 * k >= skip_hi))
         for (int r = r0; r < r1; ++r) reinterpret_cast<float4*>(x + (int64_t)r * x_stride)[k] = res;
     }
   } else {
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
       for (int r = r0 + 1; r < r1; ++r) s = s + (double)x[(int64_t)r * x_stride + k] * w[r];
       const float res = (float)(s / scl);
       if (out) out[(int64_t)c * out_stride + k] = res;
-      if (broadcast)
+      if (broadcast && (k < skip_lo || k >= skip_hi))
         for (int r = r0; r < r1; ++r) x[(int64_t)r * x_stride + k] = res;
     }
   }
@@ -64,14 +64,16 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
 
 }  // namespace
 
-extern "C" int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, const double* w,
-                                     const double* scale, int n_coalitions, int64_t n_param, float* out,
-                                     int64_t out_stride, int broadcast, void* stream) {
+namespace {
+int fedavg_launch(float* x, int64_t x_stride, const int32_t* first, const double* w, const double* scale,
+                  int n_coalitions, int64_t n_param, float* out, int64_t out_stride, int broadcast, int64_t skip_lo,
+                  int64_t skip_hi, void* stream) {
   if (x == nullptr || first == nullptr || w == nullptr || scale == nullptr) return MPLC_E_ARG;
   if (n_coalitions < 1 || n_coalitions > 65535 || n_param < 1 || x_stride < n_param) return MPLC_E_ARG;
   if (out == nullptr && !broadcast) return MPLC_E_ARG;
   if (out != nullptr && out_stride < n_param) return MPLC_E_ARG;
-  const bool vec4 = ((n_param & 3) == 0) && ((x_stride & 3) == 0) && (((uintptr_t)x & 15) == 0) &&
+  if (skip_lo < 0 || skip_hi < skip_lo || skip_hi > n_param) return MPLC_E_ARG;
+  const bool vec4 = ((skip_lo | skip_hi) & 3) == 0 && ((n_param & 3) == 0) && ((x_stride & 3) == 0) && (((uintptr_t)x & 15) == 0) &&
                     (out == nullptr || (((out_stride & 3) == 0) && (((uintptr_t)out & 15) == 0)));
   const int64_t work = vec4 ? (n_param >> 2) : n_param;
   int64_t bx = (work + TPB - 1) / TPB;
@@ -80,7 +82,22 @@ extern "C" int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* 
   if (bx > cap) bx = cap < 1 ? 1 : cap;
   dim3 grid((unsigned)bx, (unsigned)n_coalitions);
   fedavg_kernel<<<grid, TPB, 0, (hipStream_t)stream>>>(x, x_stride, first, w, scale, n_param, out, out_stride,
-                                                       broadcast, vec4 ? 1 : 0);
+                                                       broadcast, skip_lo, skip_hi, vec4 ? 1 : 0);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? MPLC_OK : (int)e;
+}
+}  // namespace
+
+extern "C" int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, const double* w,
+                                     const double* scale, int n_coalitions, int64_t n_param, float* out,
+                                     int64_t out_stride, int broadcast, void* stream) {
+  return fedavg_launch(x, x_stride, first, w, scale, n_coalitions, n_param, out, out_stride, broadcast, 0, 0, stream);
+}
+
+extern "C" int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, const int32_t* first, const double* w,
+                                                const double* scale, int n_coalitions, int64_t n_param, float* out,
+                                                int64_t out_stride, int64_t skip_lo, int64_t skip_hi, void* stream) {
+  if (out == nullptr) return MPLC_E_ARG;  // the skipped range's only copy is the coalition row
+  return fedavg_launch(x, x_stride, first, w, scale, n_coalitions, n_param, out, out_stride, 1, skip_lo, skip_hi,
+                       stream);
 }

@@ -150,7 +150,8 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
                                 const int32_t* __restrict__ rows, const int32_t* __restrict__ splits,
                                 const int32_t* __restrict__ seq, int step,
                                 int M, int round_len, int epochs, int32_t* __restrict__ idx,
-                                int32_t* __restrict__ cnt, int32_t* __restrict__ adam_t) {
+                                int32_t* __restrict__ cnt, int32_t* __restrict__ adam_t,
+                                const int32_t* __restrict__ rep_glob, int32_t* __restrict__ w3src) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)n_rep * bmax) return;
   const int r = (int)(gid / bmax);
@@ -164,6 +165,8 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
     // lookup, only the step's count and Adam iteration)
     const SlotSched nx = schedule_slot(reps[r], bmax, step + 1, M, round_len, epochs, rows, splits, seq);
     adam_t[r] = at | ((at > 0 && nx.at != at + 1) ? ADAM_LAST : 0);
+    // a FedAvg partner's first step of a round starts from the coalition model: W3 from its glob row
+    if (w3src) w3src[r] = (reps[r].kind == MPLC_REP_FEDAVG && at == 1) ? rep_glob[r] : -1;
   }
 }
 
@@ -396,7 +399,8 @@ constexpr int DF_K = 64;
 __global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict__ A, int64_t a_rstride,
                                                         const int32_t* __restrict__ cnt, int cnt_all, int bmax,
                                                         const float* __restrict__ params, int64_t stride,
-                                                        float* __restrict__ H) {
+                                                        const float* __restrict__ glob,
+                                                        const int32_t* __restrict__ w3src, float* __restrict__ H) {
   __shared__ float a_s[32 * (DF_K + 1)];
   const int r = blockIdx.y;
   const int m0 = blockIdx.x * 32;
@@ -407,7 +411,8 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict_
   const int n0 = wave * 32;
   const int kh = lane >> 5;
   const float* Ar = A + (int64_t)r * a_rstride;
-  const float* W = params + (int64_t)r * stride + OFF_W3;
+  const int gsrc = w3src ? w3src[r] : -1;  // W3 of a round's first step: the coalition row (not broadcast)
+  const float* W = (gsrc >= 0 ? glob + (int64_t)gsrc * stride : params + (int64_t)r * stride) + OFF_W3;
   floatx16 acc = zero16();
   // software pipeline over K chunks: the next chunk's A tile (8 values per thread) and W3 column slice
   // (32 values per lane) are loaded into registers while this chunk's 32 MFMAs run, so neither the LDS
@@ -623,7 +628,8 @@ constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
-    float* __restrict__ adam_v, int64_t stride, float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
+    float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
   __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
   __shared__ float p_s[D1_SCHUNK * D1_ROWS];
   const int64_t lb = xcd_block();  // logical block (slice, r), replica-major: dh and p stay in one L2
@@ -643,6 +649,9 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   const bool fresh = cfg.reset, second = (cfg.t == 2);
   const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID;
   fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c8;
+  // a round's first step reads W3 from the coalition row (the aggregation did not broadcast it)
+  const int gsrc = w3src ? w3src[r] : -1;
+  const fvec4* Wsrc = gsrc >= 0 ? reinterpret_cast<const fvec4*>(glob + roff + (int64_t)(gsrc - r) * stride) + c8 : W;
   fvec4* Mr = reinterpret_cast<fvec4*>(adam_m + roff) + c8;
   fvec4* Vr = reinterpret_cast<fvec4*>(adam_v + roff) + c8;
   const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -650,7 +659,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   fvec4 w[4], g[4], mv[4], vv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    w[i] = W[8 * i];
+    w[i] = Wsrc[8 * i];
     g[i] = z4;
     mv[i] = z4;
     vv[i] = z4;
@@ -1365,13 +1374,15 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
       !t->w1_part || !t->w2_part || !t->w2t)
     return MPLC_E_ARG;
   if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
+  if (t->glob && (!t->rep_glob || !t->w3src)) return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int R = t->n_rep, B = t->bmax;
   const int64_t S = MPLC_CNN_STRIDE;
   const int64_t slots = (int64_t)R * B;
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
-                                                                   t->idx, t->cnt, t->adam_t);
+                                                                   t->idx, t->cnt, t->adam_t, t->rep_glob,
+                                                                   t->glob ? t->w3src : nullptr);
   // t->w2t holds W2 in Winograd form for the forward, then the rotated kernel's Winograd form for the dgrad
   winograd_w2_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(1);
@@ -1379,8 +1390,9 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                          t->pooled, t->code);
   PROF_END(1);
   PROF_BEGIN(2);
+  const int32_t* w3src = t->glob ? t->w3src : nullptr;
   dense_fwd_kernel<<<dim3((B + 31) / 32, R), 256, 0, s>>>(t->pooled, (int64_t)B * FEAT, t->cnt, 0, B, t->params, S,
-                                                          t->hidden);
+                                                          t->glob, w3src, t->hidden);
   PROF_END(2);
   PROF_BEGIN(3);
   head_kernel<<<R, 256, 0, s>>>(t->hidden, t->idx, t->labels, t->cnt, t->adam_t, B, t->params, t->adam_m, t->adam_v,
@@ -1388,7 +1400,8 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   PROF_END(3);
   PROF_BEGIN(4);
   dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
-                                                                  t->params, t->adam_m, t->adam_v, S, t->dpooled,
+                                                                  t->params, t->adam_m, t->adam_v, S, t->glob,
+                                                                  w3src, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
   PROF_END(4);
   winograd_w2r_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
@@ -1421,7 +1434,7 @@ int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const f
     conv_fwd_kernel<<<dim3(FWD_PARTS, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
                                                                   w2_wino, pooled, nullptr);
     dense_fwd_kernel<<<dim3((cn + 31) / 32, n_models), 256, 0, s>>>(pooled, (int64_t)chunk * FEAT, nullptr, cn, chunk,
-                                                                    params, stride, hidden);
+                                                                    params, stride, nullptr, nullptr, hidden);
     eval_head_kernel<<<n_models, 256, 0, s>>>(hidden, cn, chunk, labels, s0, params, stride, correct, loss_sum);
     const int st = launch_status();
     if (st) return st;

@@ -23,6 +23,8 @@ SIGNATURES = {
     "mplc_shapley_exact": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mplc_fedavg_aggregate": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p,
                                       c_int64, c_int, c_void_p]),
+    "mplc_fedavg_aggregate_bcast_skip": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int64,
+                                                 c_void_p, c_int64, c_int64, c_int64, c_void_p]),
     # Monte-Carlo Shapley permutation walks over a dense table (csrc/mc_shapley.hip)
     "mplc_tmc_walk": (c_int, [c_void_p, c_int, c_void_p, c_int, ctypes.c_double, ctypes.c_double, c_int, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -77,7 +77,8 @@ class TrainT(ctypes.Structure):
                 ("w2_part", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("pad1", ctypes.c_int32),
-                ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p), ("hstats", ctypes.c_void_p)]
+                ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p), ("hstats", ctypes.c_void_p),
+                ("glob", ctypes.c_void_p), ("rep_glob", ctypes.c_void_p), ("w3src", ctypes.c_void_p)]
 
 KERNEL_IDS = {"conv_fwd": 1, "dense_fwd": 2, "head": 3, "dense1_bwd_adam": 4, "conv_bwd_data": 5, "conv_wgrad": 6,
               "adam_small": 7}
@@ -177,6 +178,9 @@ class MnistModel:
     KERAS_LAYERS = KERAS_LAYERS
     KERNEL_IDS = KERNEL_IDS
     input_shape = (28, 28)
+    # FedAvg aggregation leaves W3 (98 % of the parameters) out of the broadcast: a round's first step reads
+    # it from the coalition row (mplc_cnn_train_t.glob, mplc_fedavg_aggregate_bcast_skip)
+    BCAST_SKIP = (KERAS_LAYERS[4][0], KERAS_LAYERS[5][0])
 
     def __init__(self):
         _bind()
@@ -204,7 +208,8 @@ class MnistModel:
             pooled=torch.empty((R, B, FEAT), **f32), code=torch.empty((R, B, FEAT), dtype=torch.uint8, device=dev),
             hidden=torch.empty((R, B, HID), **f32), dhidden=torch.empty((R, B, HID), **f32),
             dpooled=torch.empty((R, B, FEAT), **f32), w1_part=torch.empty((R, B, W1_BANDS, W1P), **f32),
-            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, W2T), **f32))
+            w2_part=torch.empty((R, splits, W2P), **f32), w2t=torch.empty((R, W2T), **f32),
+            w3src=torch.empty(R, **i32))
         t = TrainT()
         t.n_rep, t.bmax, t.w2_splits = R, B, splits
         t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
@@ -215,6 +220,8 @@ class MnistModel:
         for k, v in st.ws.items():
             setattr(t, k, v.data_ptr())
         t.lr, t.beta1, t.beta2, t.eps = 0.001, 0.9, 0.999, 1e-7
+        if not st.seq_mode:  # FedAvg rounds start from the coalition row (W3 is not broadcast)
+            t.glob, t.rep_glob = st.glob.data_ptr(), st.src_map.data_ptr()
         st.t = t
 
     def free(self, st):
@@ -358,6 +365,7 @@ class TrainBatch:
                                          dtype=np.uint64).view(np.int64)).to(dev)
         self.model.init_params(self.glob, keys, self.stream)
         src_map = torch.tensor(src, **i32)
+        self.src_map = src_map  # replica -> coalition row of glob
         _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), S,
                                              _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
         self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
@@ -439,11 +447,18 @@ class TrainBatch:
         for (r0, c0, nc, first, w, sc) in self.run_args:
             if aggregate_now:
                 x = self.params[r0:] if not self.seq_mode else self.snap[self.snap_row(c0):]
-                _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(x), S, _native.ptr(first), _native.ptr(w),
-                                                             _native.ptr(sc), nc, NP,
-                                                             _native.ptr(self.glob[c0:c0 + nc]), S,
-                                                             0 if self.seq_mode else 1, self.stream),
-                              "mplc_fedavg_aggregate")
+                skip = None if self.seq_mode else getattr(self.model, "BCAST_SKIP", None)
+                if skip is not None:  # the next round's first step reads this range from glob
+                    _native.check(self.lib.mplc_fedavg_aggregate_bcast_skip(
+                        _native.ptr(x), S, _native.ptr(first), _native.ptr(w), _native.ptr(sc), nc, NP,
+                        _native.ptr(self.glob[c0:c0 + nc]), S, skip[0], skip[1], self.stream),
+                        "mplc_fedavg_aggregate_bcast_skip")
+                else:
+                    _native.check(self.lib.mplc_fedavg_aggregate(_native.ptr(x), S, _native.ptr(first), _native.ptr(w),
+                                                                 _native.ptr(sc), nc, NP,
+                                                                 _native.ptr(self.glob[c0:c0 + nc]), S,
+                                                                 0 if self.seq_mode else 1, self.stream),
+                                  "mplc_fedavg_aggregate")
                 if self.seq_mode:  # the averaged model continues training
                     self._rows_copy(self.params[r0:r0 + nc], self.glob, list(range(c0, c0 + nc)))
             else:  # sequential without averaging: the coalition model as it stands

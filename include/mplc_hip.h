@@ -81,6 +81,14 @@ int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, cons
                           const double* scale, int n_coalitions, int64_t n_param, float* out,
                           int64_t out_stride, int broadcast, void* stream);
 
+/* As mplc_fedavg_aggregate with broadcast, except that parameters [skip_lo, skip_hi) are not written back
+ * into the replica rows: their only copy is out[c] (required), which the next round's first step reads
+ * instead (the MNIST trainer's W3, include/mplc_hip_cnn.h `glob` / `rep_glob`): 98 % of the broadcast bytes
+ * of a FedAvg round are not written, and the replicas of a coalition read one shared row. */
+int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, const int32_t* first, const double* w,
+                                     const double* scale, int n_coalitions, int64_t n_param, float* out,
+                                     int64_t out_stride, int64_t skip_lo, int64_t skip_hi, void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Batched FedAvg logistic regression (Titanic model, BASELINE config #2), one workgroup per coalition.
  * Replaces, per coalition, FederatedAverageLearning.fit (mplc/multi_partner_learning.py:195-216,

@@ -126,6 +126,13 @@ typedef struct {
    * update, correct predictions, samples] - the running 'loss' / 'accuracy' that a Keras fit reports
    * (mplc/multi_partner_learning.py:130-133 log_partner_perf); idle replicas write zeros */
   double* hstats;         /* [n_rep][3]                                                   */
+  /* optional (NULL = off): FedAvg replicas read W3 at the first step of a round (Adam t = 1) from their
+   * coalition's row of glob instead of their own row, which the round's aggregation then need not
+   * overwrite (mplc_fedavg_aggregate_bcast_skip with [MPLC_CNN_OFF_W3, MPLC_CNN_OFF_B3)).  The step
+   * writes the updated W3 into the replica's own row as usual. */
+  const float* glob;      /* [n_coalitions][MPLC_CNN_STRIDE] coalition models                    */
+  const int32_t* rep_glob;  /* [n_rep] replica -> its coalition's row of glob                 */
+  int32_t* w3src;         /* [n_rep] workspace: glob row W3 is read from this step, or -1      */
 } mplc_cnn_train_t;
 
 /* Parameter row stride in floats (== MPLC_CNN_STRIDE). */

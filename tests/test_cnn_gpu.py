@@ -177,8 +177,13 @@ def test_fedavg_aggregation_inside_training_is_np_average(scenario, engine):
     ref = np.average(before[:, :ocnn.STRIDE], axis=0, weights=w).astype(np.float32)
     assert np.array_equal(st.glob.cpu().numpy()[0], ref)
     after = st.params.cpu().numpy()
-    for r in range(3):
-        assert np.array_equal(after[r], ref)  # broadcast: every partner starts the next round from it
+    lo, hi = st.model.BCAST_SKIP  # W3: not broadcast, the next round's first step reads the coalition row
+    for r in range(3):  # broadcast: every partner starts the next round from the average
+        assert np.array_equal(after[r][:lo], ref[:lo]) and np.array_equal(after[r][hi:], ref[hi:])
+        assert np.array_equal(after[r][lo:hi], before[r][lo:hi])
+    st.step(st.round_len)  # first step of round 2: every replica sources W3 from coalition row 0
+    torch.cuda.synchronize()
+    assert st.ws["w3src"].cpu().tolist() == [0, 0, 0]
 
 
 def test_values_independent_of_batch_composition(engine):
