@@ -758,9 +758,9 @@ __global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restri
                                                            const int32_t* __restrict__ cnt, float* __restrict__ Ur) {
   const int r = blockIdx.y;
   if (cnt && cnt[r] == 0) return;
-  const int e = blockIdx.x * 256 + threadIdx.x;  // (co, ci) of the output
+  const int e = blockIdx.x * 256 + threadIdx.x;  // (ci, co): consecutive lanes read consecutive co of W2
   if (e >= C1 * C2) return;
-  const int co = e / C1, ci = e % C1;
+  const int ci = e / C2, co = e % C2;
   const float* W2 = params + (int64_t)r * stride + OFF_W2 + ci * C2 + co;  // tap k at W2[k * C1 * C2]
   float g[3][3];
 #pragma unroll
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
   }
-  fvec4* U = reinterpret_cast<fvec4*>(Ur + (int64_t)r * MPLC_CNN_W2T + (int64_t)e * 16);
+  fvec4* U = reinterpret_cast<fvec4*>(Ur + (int64_t)r * MPLC_CNN_W2T + (int64_t)(co * C1 + ci) * 16);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float o[4];
@@ -1267,8 +1267,18 @@ __global__ void adam_small_kernel(const int32_t* __restrict__ cnt, const int32_t
   if (e >= OFF_W3) return;
   float g = 0.0f;
   if (e < OFF_W2) {
+    // (sample, band) order; the partials' loads issued 16 at a time ahead of their (sequential) adds
     const float* w = w1_part + (int64_t)r * bmax * BWD_BANDS * MPLC_CNN_W1P + e;
-    for (int jj = 0; jj < BWD_BANDS * count; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];  // (sample, band) order
+    const int n = BWD_BANDS * count;
+    int jj = 0;
+    for (; jj + 16 <= n; jj += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = w[(int64_t)(jj + u) * MPLC_CNN_W1P];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) g += v[u];
+    }
+    for (; jj < n; ++jj) g += w[(int64_t)jj * MPLC_CNN_W1P];
   } else {
     const float* w = w2_part + (int64_t)r * splits * MPLC_CNN_W2P + (e - OFF_W2);
     const int used = (count + WG_SAMPLES - 1) / WG_SAMPLES;
