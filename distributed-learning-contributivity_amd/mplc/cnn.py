@@ -239,33 +239,44 @@ class MnistModel:
             st.t.prof_kernel, st.t.prof_begin, st.t.prof_end = 0, None, None
         _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(st.t), st.stream), "mplc_cnn_train_step")
         if prof is not None and prof.want_stash:
-            prof.stash_step(st.ws["cnt"], st.ws["adam_t"])
+            prof.stash_step(st.ws["cnt"], st.ws["adam_t"], st.ws["w3src"])
 
     @staticmethod
     def algorithmic_units(stash):
-        """Algorithmic work of the timed steps from their stashed schedules [(cnt, adam_t)], per kernel:
+        """Algorithmic work of the timed steps from their stashed schedules [(cnt, adam_t, w3src)], per kernel:
         samples (the convolution kernels' unit) and the HBM bytes the two W3 kernels must move
         (csrc/mnist_cnn.hip dense_fwd_kernel / dense1_bwd_adam_kernel):
           dense_fwd:       W3 read + per sample its pooled row read and hidden row written;
           dense1_bwd_adam: W3 read and written; Adam moments by the optimizer step t - t = 1 writes the
                            gradient into the m slot, t = 2 reads it and writes m and v, t >= 3 reads and
                            writes m and v, the optimizer's last step writes no moments; per sample the pooled
-                           row and dh read, the dpooled row written."""
+                           row and dh read, the dpooled row written.
+        A FedAvg round's first step reads W3 from the coalition row (w3src >= 0), shared by the coalition's
+        replicas: that row counts once per coalition, not once per replica."""
         import torch
         if not stash:
             return {}
-        cnt = torch.stack([c for c, _ in stash]).to(torch.float64)
-        at = torch.stack([a for _, a in stash])
+        cnt = torch.stack([e[0] for e in stash]).to(torch.float64)
+        at = torch.stack([e[1] for e in stash])
+        src = torch.stack([e[2] for e in stash])
+        # distinct coalition rows read per step (rows are < 2^20; steps are offset so rows never collide)
+        steps = torch.arange(src.shape[0], device=src.device, dtype=torch.int64).unsqueeze(1)
+        shared = src >= 0
+        keys = (steps * (1 << 20) + src.to(torch.int64))[shared & (cnt > 0)]
+        n_shared_rows = float(torch.unique(keys).numel())
         t = at & (ADAM_LAST - 1)
         last = (at & ADAM_LAST) != 0
         act = (cnt > 0).to(torch.float64)
         w3 = float(FEAT * HID * 4)
         mom_rd = torch.where(t == 1, 0.0, torch.where(t == 2, 1.0, 2.0)).to(torch.float64)
         mom_wr = torch.where(last, 0.0, torch.where(t == 1, 1.0, 2.0)).to(torch.float64)
-        d1 = act * (w3 * (2.0 + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
-        df = act * (w3 + cnt * float(FEAT * 4 + HID * 4))
-        return {"samples": float(cnt.sum().item()), "dense1_bwd_adam_bytes": float(d1.sum().item()),
-                "dense_fwd_bytes": float(df.sum().item())}
+        own = (~shared).to(torch.float64)  # replicas reading W3 from their own row
+        d1 = act * (w3 * (1.0 + own + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
+        df = act * (w3 * own + cnt * float(FEAT * 4 + HID * 4))
+        shared_w3 = n_shared_rows * w3
+        return {"samples": float(cnt.sum().item()),
+                "dense1_bwd_adam_bytes": float(d1.sum().item()) + shared_w3,
+                "dense_fwd_bytes": float(df.sum().item()) + shared_w3}
 
     def evaluate(self, eng, sel, x, y):
         """(correct counts, mean CE) of the C models in `sel` [C][STRIDE] on (x, y)."""

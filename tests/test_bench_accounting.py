@@ -22,7 +22,8 @@ def test_dense_bytes_follow_adam_schedule():
     # replicas: fresh step (t=1), idle, step 2, step 5, last step of an optimizer (t=8), t=1 that is also last
     cnt = torch.tensor([27, 0, 27, 10, 27, 5], dtype=torch.int32)
     at = torch.tensor([1, 0, 2, 5, 8 | L, 1 | L], dtype=torch.int32)
-    u = cnn.MnistModel.algorithmic_units([(cnt, at)])
+    src = torch.full((6,), -1, dtype=torch.int32)
+    u = cnn.MnistModel.algorithmic_units([(cnt, at, src)])
     per_sample_bwd = 2 * 9216 * 4 + 128 * 4
     # W3 read+write (2) + moments: t1 -> write g (1); t2 -> read g, write m, v (3); t5 -> 4; last t8 -> read 2;
     # t1 last -> nothing
@@ -52,3 +53,15 @@ def test_kernel_table_picks_rates():
     assert cb["achieved"] == pytest.approx(1000 * bench.CONV_BWD_DATA_FLOP_PER_SAMPLE / 0.01 / 1e12, abs=0.01)
     assert "frac" not in tab["head"]
     assert sum(e["time_share"] for e in tab.values()) == pytest.approx(1.0, abs=1e-3)
+
+
+def test_shared_coalition_rows_count_once():
+    """A FedAvg round's first step: the replicas of a coalition read W3 from one coalition row."""
+    cnt = torch.tensor([27, 27, 27, 10], dtype=torch.int32)
+    at = torch.tensor([1, 1, 1, 1], dtype=torch.int32)
+    src = torch.tensor([4, 4, 4, 7], dtype=torch.int32)  # coalition 4 has three partners, coalition 7 one
+    u = cnn.MnistModel.algorithmic_units([(cnt, at, src)])
+    per_sample_bwd = 2 * 9216 * 4 + 128 * 4
+    # W3 write + g write per replica, two distinct coalition rows read
+    assert u["dense1_bwd_adam_bytes"] == 4 * 2 * W3 + 91 * per_sample_bwd + 2 * W3
+    assert u["dense_fwd_bytes"] == 91 * (9216 * 4 + 128 * 4) + 2 * W3
