@@ -112,3 +112,37 @@ def test_fedavg_aggregate_bit_exact_vs_np_average():
             xt = torch.from_numpy(x).cuda()
             out = fedavg_aggregate([xt], [list(range(P))], [sizes], scheme=scheme)[0].cpu().numpy()
             assert np.array_equal(out, ref), (sizes, scheme)
+
+
+def test_fedavg_bcast_skip_leaves_range_in_the_replicas():
+    """mplc_fedavg_aggregate_bcast_skip: the average in the coalition row, written back into every replica row
+    except [skip_lo, skip_hi) (the MNIST W3, which the next round's first step reads from the coalition row)."""
+    import torch
+    from mplc import _native
+    from mplc.fedavg import aggregation_weights
+    rng = np.random.default_rng(1)
+    sizes = [874, 2186, 1312]
+    P, n_param, stride = 3, 1199882, 1199936
+    x = np.zeros((P, stride), dtype=np.float32)
+    x[:, :n_param] = rng.normal(scale=0.05, size=(P, n_param))
+    w, scl = aggregation_weights(sizes, "data-volume")
+    ref = np.average(x[:, :n_param], axis=0, weights=np.asarray(w)).astype(np.float32)
+    xt = torch.from_numpy(x).cuda()
+    out = torch.zeros((1, stride), dtype=torch.float32, device="cuda")
+    first = torch.tensor([0, P], dtype=torch.int32, device="cuda")
+    wt = torch.tensor(w, dtype=torch.float64, device="cuda")
+    st = torch.tensor([scl], dtype=torch.float64, device="cuda")
+    lo, hi = 18816, 1198464
+    _native.check(_native.lib().mplc_fedavg_aggregate_bcast_skip(
+        _native.ptr(xt), stride, _native.ptr(first), _native.ptr(wt), _native.ptr(st), 1, n_param,
+        _native.ptr(out), stride, lo, hi, _native.stream_handle()), "mplc_fedavg_aggregate_bcast_skip")
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy()[0, :n_param], ref)
+    after = xt.cpu().numpy()
+    for r in range(P):
+        assert np.array_equal(after[r, :lo], ref[:lo]) and np.array_equal(after[r, hi:n_param], ref[hi:])
+        assert np.array_equal(after[r, lo:hi], x[r, lo:hi])
+    # without an output row the skipped range would be lost: refused
+    assert _native.lib().mplc_fedavg_aggregate_bcast_skip(
+        _native.ptr(xt), stride, _native.ptr(first), _native.ptr(wt), _native.ptr(st), 1, n_param,
+        None, stride, lo, hi, _native.stream_handle()) != 0
