@@ -155,7 +155,8 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
                                 const int32_t* __restrict__ seq, int step,
                                 int M, int round_len, int epochs, int32_t* __restrict__ idx,
                                 int32_t* __restrict__ cnt, int32_t* __restrict__ opt_t,
-                                uint64_t* __restrict__ drop_key) {
+                                uint64_t* __restrict__ drop_key, const int32_t* __restrict__ rep_glob,
+                                int32_t* __restrict__ w5src) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)n_rep * bmax) return;
   const int r = (int)(gid / bmax);
@@ -166,6 +167,8 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
     cnt[r] = ss.c;
     opt_t[r] = ss.at;
     drop_key[r] = ss.dkey;
+    // a FedAvg partner's first step of a round starts from the coalition model: W5 from its glob row
+    if (w5src) w5src[r] = (reps[r].kind == MPLC_REP_FEDAVG && ss.at == 1) ? rep_glob[r] : -1;
   }
 }
 
@@ -687,7 +690,9 @@ constexpr int DF_K = 64;
 
 __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict__ A, const int32_t* __restrict__ cnt,
                                                          int cnt_all, int bmax, const float* __restrict__ params,
-                                                         int64_t stride, const uint64_t* __restrict__ drop_key,
+                                                         int64_t stride, const float* __restrict__ glob,
+                                                         const int32_t* __restrict__ w5src,
+                                                         const uint64_t* __restrict__ drop_key,
                                                          float* __restrict__ H, uint8_t* __restrict__ code) {
   __shared__ float a_s[32 * (DF_K + 1)];
   const int r = blockIdx.z;
@@ -699,7 +704,8 @@ __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict
   const int n0 = blockIdx.y * 128 + wave * 32;
   const int kh = lane >> 5;
   const float* Ar = A + (int64_t)r * bmax * FEAT;
-  const float* W = params + (int64_t)r * stride + OFF_W5;
+  const int gsrc = w5src ? w5src[r] : -1;  // W5 of a round's first step: the coalition row (not broadcast)
+  const float* W = (gsrc >= 0 ? glob + (int64_t)gsrc * stride : params + (int64_t)r * stride) + OFF_W5;
   floatx16 acc = zero16();
   // software pipeline over K chunks: the next chunk's A tile (8 values per thread) and W5 column slice
   // (32 values per lane) load into registers while this chunk's 32 MFMAs run
@@ -891,7 +897,8 @@ constexpr int D5_SCHUNK = 16;   // samples staged at a time
 __global__ __launch_bounds__(256) void dense5_bwd_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
     const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
-    float* __restrict__ rms, float* __restrict__ dZ4, float lr, float rho, float omr, float decay, float eps) {
+    float* __restrict__ rms, const float* __restrict__ glob, const int32_t* __restrict__ w5src,
+    float* __restrict__ dZ4, float lr, float rho, float omr, float decay, float eps) {
   constexpr int KB = D5_ROWS * D5_GROUPS;
   __shared__ fvec4 dh_s[D5_SCHUNK * (HID / 4)];
   __shared__ float p_s[D5_SCHUNK * KB];
@@ -925,11 +932,19 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
   };
   // software pipeline: the next row group's W5 / accumulator loads are in flight while this one computes
   fvec4 w[4], av[4], wn[4], avn[4];
+  // a round's first step reads W5 from the coalition row (the aggregation did not broadcast it); the update is
+  // written into the replica's own row
+  const int gsrc = w5src ? w5src[r] : -1;
+  const int64_t src_shift = gsrc >= 0 ? (int64_t)(gsrc - r) * STRIDE : 0;
+  auto wsrc = [&](const fvec4* Wp) {
+    return gsrc >= 0 ? reinterpret_cast<const fvec4*>(glob + (reinterpret_cast<const float*>(Wp) - params) + src_shift)
+                     : Wp;
+  };
   fvec4 *W, *Ra;
   row_ptrs(0, W, Ra);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    w[i] = W[32 * i];
+    w[i] = wsrc(W)[32 * i];
     av[i] = cfg.reset ? z4 : __builtin_nontemporal_load(Ra + 32 * i);
   }
   if (one_chunk) {
@@ -942,7 +957,7 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
       row_ptrs(grp + 1, Wn, Ran);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        wn[i] = Wn[32 * i];
+        wn[i] = wsrc(Wn)[32 * i];
         avn[i] = cfg.reset ? z4 : __builtin_nontemporal_load(Ran + 32 * i);
       }
     }
@@ -1106,7 +1121,8 @@ ConvArgs conv_args(const float* in, int in_mode, int row_base, const int32_t* id
 void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, int row_base, const int32_t* idx,
                      const int32_t* cnt, int cnt_all, const float* params, int64_t stride, const uint64_t* drop_key,
                      float* a1, float* d2, uint8_t* code2, float* a3, float* d4, uint8_t* code4, float* h5,
-                     uint8_t* code5, int prof, void* pb, void* pe) {
+                     uint8_t* code5, int prof, void* pb, void* pe, const float* glob = nullptr,
+                     const int32_t* w5src = nullptr) {
 #define PB(k) \
   if (prof == (k) && pb) (void)hipEventRecord((hipEvent_t)pb, s)
 #define PE(k) \
@@ -1146,8 +1162,8 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   CONV4_FWD<<<dim3(1, B, R), 192, 0, s>>>(c4);
   PE(4);
   PB(5);
-  dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, drop_key,
-                                                                      h5, code5);
+  dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, glob,
+                                                                      w5src, drop_key, h5, code5);
   PE(5);
 #undef PB
 #undef PE
@@ -1178,21 +1194,26 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
       !t->code5 || !t->dh5 || !t->dz4 || !t->dz3 || !t->dz2 || !t->dz1 || !t->wt || !t->wpart)
     return MPLC_E_ARG;
   if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
+  if (t->glob && (!t->rep_glob || !t->w5src)) return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int R = t->n_rep, B = t->bmax;
   const int64_t slots = (int64_t)R * B;
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
-                                                                   t->idx, t->cnt, t->opt_t, t->drop_key);
+                                                                   t->idx, t->cnt, t->opt_t, t->drop_key,
+                                                                   t->rep_glob, t->glob ? t->w5src : nullptr);
+  const int32_t* w5src = t->glob ? t->w5src : nullptr;
   enqueue_forward(s, R, B, t->x, 1, 0, t->idx, t->cnt, 0, t->params, STRIDE, t->drop_key, t->a1, t->d2, t->code2,
-                  t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end);
+                  t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end, t->glob,
+                  w5src);
   PROF_BEGIN(6);
   head_kernel<<<R, 256, 0, s>>>(t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5,
                                 t->lr, t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
   PROF_END(6);
   PROF_BEGIN(7);
   dense5_bwd_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
-                                                            t->rms, t->dz4, t->lr, t->rho, t->one_minus_rho, t->decay, t->eps);
+                                                            t->rms, t->glob, w5src, t->dz4, t->lr, t->rho,
+                                                            t->one_minus_rho, t->decay, t->eps);
   PROF_END(7);
   transpose_w_kernel<<<dim3(32, R), 256, 0, s>>>(t->params, t->cnt, t->wt);
   const int SP = t->wg_splits;

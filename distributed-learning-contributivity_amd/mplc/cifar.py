@@ -42,7 +42,8 @@ class CifarTrainT(ctypes.Structure):
                                                    "wpart")]
                 + [(n, ctypes.c_float) for n in ("lr", "rho", "one_minus_rho", "decay", "eps")]
                 + [("prof_kernel", ctypes.c_int32), ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p),
-                   ("hstats", ctypes.c_void_p)])
+                   ("hstats", ctypes.c_void_p), ("glob", ctypes.c_void_p), ("rep_glob", ctypes.c_void_p),
+                   ("w5src", ctypes.c_void_p)])
 
 
 _BOUND = False
@@ -69,6 +70,9 @@ class CifarModel:
                     (1245824, (512, 10)), (1250944, (10,)))
     KERNEL_IDS = KERNEL_IDS
     input_shape = (32, 32, 3)
+    # FedAvg aggregation leaves W5 (94 % of the parameters) out of the broadcast: a round's first step reads
+    # it from the coalition row (mplc_cifar_train_t.glob, mplc_fedavg_aggregate_bcast_skip)
+    BCAST_SKIP = (KERAS_LAYERS[8][0], KERAS_LAYERS[9][0])
     # Keras 2.3.1 RMSprop(learning_rate=0.0001, decay=1e-6): rho 0.9, epsilon K.epsilon() = 1e-7
     lr, rho, decay, eps = 1e-4, 0.9, 1e-6, 1e-7
 
@@ -101,7 +105,7 @@ class CifarModel:
             d5=torch.empty((R, B, H5), **f32), code5=torch.empty((R, B, H5), **u8), dh5=torch.empty((R, B, H5), **f32),
             dz4=torch.zeros((R, B, DZ4), **f32), dz3=torch.empty((R, B, DZ3), **f32),
             dz2=torch.empty((R, B, DZ2), **f32), dz1=torch.empty((R, B, DZ1), **f32),
-            wt=torch.empty((R, WT), **f32), wpart=torch.empty((R, splits, WPART), **f32))
+            wt=torch.empty((R, WT), **f32), wpart=torch.empty((R, splits, WPART), **f32), w5src=torch.empty(R, **i32))
         t = CifarTrainT()
         t.n_rep, t.bmax, t.wg_splits = R, B, splits
         t.minibatch_count, t.round_len, t.epochs = eng.minibatch_count, st.round_len, st.epochs
@@ -113,6 +117,8 @@ class CifarModel:
             setattr(t, k, v.data_ptr())
         t.lr, t.rho, t.decay, t.eps = self.lr, self.rho, self.decay, self.eps
         t.one_minus_rho = float(np.float32(1.0 - self.rho))  # Keras: (1. - rho) on the Python double
+        if not st.seq_mode:  # FedAvg rounds start from the coalition row (W5 is not broadcast)
+            t.glob, t.rep_glob = st.glob.data_ptr(), st.src_map.data_ptr()
         st.t = t
 
     def free(self, st):

@@ -115,6 +115,12 @@ typedef struct {
    * update, correct predictions, samples] (dropout active, as a Keras fit reports them); see
    * mplc_cnn_train_t.hstats */
   double* hstats;         /* [n_rep][3]                                                   */
+  /* optional (NULL = off), as mplc_cnn_train_t.glob for W3: FedAvg replicas read W5 at the first step of a
+   * round from their coalition's row of glob, which the aggregation then need not broadcast
+   * (mplc_fedavg_aggregate_bcast_skip with [MPLC_CIFAR_OFF_W5, MPLC_CIFAR_OFF_B5)). */
+  const float* glob;      /* [n_coalitions][MPLC_CIFAR_STRIDE] coalition models                   */
+  const int32_t* rep_glob;  /* [n_rep] replica -> its coalition's row of glob                 */
+  int32_t* w5src;         /* [n_rep] workspace: glob row W5 is read from this step, or -1      */
 } mplc_cifar_train_t;
 
 /* Parameter row stride in floats (== MPLC_CIFAR_STRIDE). */

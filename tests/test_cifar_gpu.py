@@ -175,7 +175,14 @@ def test_fedavg_aggregation_inside_training_is_np_average(engine):
     sizes = [engine.partner_sizes[p] for p in (0, 1, 2)]
     ref = np.average(before[:, :occ.STRIDE], axis=0, weights=np.asarray(sizes) / np.sum(sizes)).astype(np.float32)
     assert np.array_equal(st.glob.cpu().numpy()[0], ref)
-    assert all(np.array_equal(st.params.cpu().numpy()[r], ref) for r in range(3))
+    after = st.params.cpu().numpy()
+    lo, hi = st.model.BCAST_SKIP  # W5: not broadcast, the next round's first step reads the coalition row
+    for r in range(3):  # broadcast: every partner starts the next round from the average
+        assert np.array_equal(after[r][:lo], ref[:lo]) and np.array_equal(after[r][hi:], ref[hi:])
+        assert np.array_equal(after[r][lo:hi], before[r][lo:hi])
+    st.step(st.round_len)  # first step of round 2: every replica sources W5 from coalition row 0
+    torch.cuda.synchronize()
+    assert st.ws["w5src"].cpu().tolist() == [0, 0, 0]
 
 
 def test_values_independent_of_batch_composition(engine):
