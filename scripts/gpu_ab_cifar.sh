@@ -1,5 +1,8 @@
 # CIFAR probe A/B between the committed tree (gpurun_ab/oldtree: package + library as of HEAD) and the working
 # tree: kernel trace of each and the v(S) hash.  bash scripts/gpu_ab_cifar.sh <probe args...>
+# Prepare the old tree on the CPU side first:
+#   git archive HEAD distributed-learning-contributivity_amd scripts/probe_train.py include | tar -x -C gpurun_ab/oldtree
+#   (then build it there, or copy a library built from HEAD into its mplc/lib/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
