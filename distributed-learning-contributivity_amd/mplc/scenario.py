@@ -30,6 +30,18 @@ PARAMS_KNOWN = ["dataset", "dataset_name", "dataset_proportion", "methods", "mul
                 "init_model_from", "is_quick_demo", "engine_seed", "coalition_values_file"]
 
 
+
+def _label_codes(y):
+    """LabelEncoder().fit_transform([str(row) for row in y]) (the reference's label encoding for the split,
+    mplc/scenario.py:573), with str() taken once per distinct row instead of once per sample: equal rows give
+    equal strings, so the codes are identical."""
+    y = np.asarray(y)
+    uniq, inverse = np.unique(y, axis=0, return_inverse=True) if y.ndim > 1 else np.unique(y, return_inverse=True)
+    inverse = np.asarray(inverse).reshape(-1)
+    names = [str(u) for u in uniq]
+    order = LabelEncoder().fit(names)
+    return order.transform(names)[inverse]
+
 class Scenario:
     def __init__(self, partners_count, amounts_per_partner, dataset=None, dataset_name=constants.MNIST,
                  dataset_proportion=1, samples_split_option=None, corrupted_datasets=None,
@@ -126,7 +138,7 @@ class Scenario:
 
     def split_data(self, is_logging_enabled=True):
         """mplc/scenario.py:571-681 (basic split), plus each partner's row indices (train_idx)."""
-        y_train = LabelEncoder().fit_transform([str(y) for y in self.dataset.y_train])
+        y_train = _label_codes(self.dataset.y_train)
         assert len(self.amounts_per_partner) == self.partners_count, \
             "Error: amounts_per_partner list should have a size equals to partners_count"
         assert np.sum(self.amounts_per_partner) == 1, \

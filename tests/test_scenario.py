@@ -129,3 +129,17 @@ def test_missing_dataset_is_an_error_not_synthetic(monkeypatch, tmp_path):
     assert dm.Mnist(synthetic=True, n_train=100, n_test=10).synthetic
     monkeypatch.setenv("MPLC_SYNTHETIC_DATA", "1")
     assert dm.Titanic().synthetic
+
+
+def test_label_codes_equal_reference_string_encoding():
+    """split_data's label codes: LabelEncoder over str(row) per sample (reference mplc/scenario.py:573),
+    computed once per distinct row."""
+    import numpy as np
+    from sklearn.preprocessing import LabelEncoder
+    from mplc.scenario import _label_codes
+    rng = np.random.default_rng(3)
+    one_hot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, 4000)]
+    ints = rng.integers(0, 2, 900)
+    for y in (one_hot, ints):
+        ref = LabelEncoder().fit_transform([str(r) for r in y])
+        assert np.array_equal(_label_codes(y), ref)
