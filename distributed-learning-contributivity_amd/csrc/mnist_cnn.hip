@@ -1054,7 +1054,10 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 // other replicas share the launch.
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_THREADS = 256;
-constexpr int WG_SAMPLES = 8;                     // samples per wgrad split (fixed: reproducible sums)
+#ifndef MPLC_WG_SAMPLES
+#define MPLC_WG_SAMPLES 9  // bs 27 (config #3) = 3 equal splits: no short split block (8 -> 8, 8, 8, 3: +18 % wgrad)
+#endif
+constexpr int WG_SAMPLES = MPLC_WG_SAMPLES;       // samples per wgrad split (fixed: reproducible sums)
 constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // (dp, code) pairs per thread per band: 2 rows x 12 x 64
 // Staged operands are read as 8-byte pairs: a lane needs channels ci and 16 + ci of a conv1 position (stored
 // adjacent: slot 2 * (ci & 15) + (ci >> 4)) and (value, argmax) of a window channel (one int2), so a k-step's
@@ -1351,6 +1354,8 @@ inline int launch_status() {
 extern "C" {
 
 int mplc_cnn_stride(void) { return MPLC_CNN_STRIDE; }
+
+int mplc_cnn_wgrad_split_samples(void) { return WG_SAMPLES; }
 
 int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
   if (!params || !keys || n_models < 1 || n_models > 65535 || stride < MPLC_CNN_NPARAM) return MPLC_E_ARG;

@@ -33,6 +33,7 @@ SIGNATURES = {
                                  ctypes.c_double, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     # batched CNN trainer (include/mplc_hip_cnn.h); mplc.cnn re-binds train_step with its struct type
     "mplc_cnn_stride": (c_int, []),
+    "mplc_cnn_wgrad_split_samples": (c_int, []),
     "mplc_cnn_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cnn_copy_rows": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cnn_train_step": (c_int, [c_void_p, c_void_p]),

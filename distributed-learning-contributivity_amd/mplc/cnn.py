@@ -28,7 +28,7 @@ W1P = 320
 W2P = 18496
 W1_BANDS = 3  # MPLC_CNN_W1_BANDS: [dW1 | db1] partials per sample (data-gradient blocks)
 W2T = 32768  # MPLC_CNN_W2T: W2 in Winograd form (forward), then transposed (data gradient)
-WG_SAMPLES = 8
+WG_SAMPLES = 9  # samples per conv2 weight-gradient split; the library's value replaces it at bind time
 ADAM_LAST = 1 << 30  # adam_t flag (csrc/mnist_cnn.hip): the optimizer's last step
 PROF_ALL = -1        # mplc_cnn_train_t.prof_kernel (MPLC_PROF_ALL): time every launch of the step
 PATIENCE = 10
@@ -100,6 +100,8 @@ def _bind():
     lib = _native.lib()
     if lib.mplc_cnn_stride() != STRIDE:
         raise RuntimeError("libmplc_hip.so CNN layout mismatch; rebuild")
+    global WG_SAMPLES
+    WG_SAMPLES = int(lib.mplc_cnn_wgrad_split_samples())  # the library's conv2 weight-gradient split size
     _BOUND = True
 
 
@@ -187,7 +189,7 @@ class MnistModel:
         self.lib = _native.lib()
 
     def replica_bytes(self, bmax):
-        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + W1_BANDS * bmax * W1P * 4 + ((bmax + 7) // 8) * W2P * 4
+        return (3 * STRIDE * 4 + bmax * FEAT * 9 + 2 * bmax * HID * 4 + W1_BANDS * bmax * W1P * 4 + ((bmax + WG_SAMPLES - 1) // WG_SAMPLES) * W2P * 4
                 + W2T * 4 + bmax * 12)
 
     def init_params(self, glob, keys, stream):

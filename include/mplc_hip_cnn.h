@@ -138,6 +138,9 @@ typedef struct {
 /* Parameter row stride in floats (== MPLC_CNN_STRIDE). */
 int mplc_cnn_stride(void);
 
+/* Samples per conv2 weight-gradient split: mplc_cnn_train_t.w2_splits must be ceil(bmax / this). */
+int mplc_cnn_wgrad_split_samples(void);
+
 /* glorot_uniform kernels / zero biases for n_models rows, keyed per model (deterministic counter RNG). */
 int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream);
 

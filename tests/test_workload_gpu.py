@@ -6,8 +6,8 @@ train as ONE lockstep batch.  Checks:
   - efficiency: sum of the Shapley values = v(N) (to 1e-12; v(empty) = 0, mplc/contributivity.py:1210-1253);
   - batch invariance: coalitions re-evaluated alone give bit-identical values to the 5120-replica batch;
   - |S| in {1, 2} coalitions against the oracle (oracle/cnn.py, sequential like the reference): no bias
-    (the mean SIGNED difference over six coalitions within 1 pt), mean |difference| within 2 pt, each within
-    4 pt (10000 test samples: 1 pt = 100 samples).  One epoch leaves the models in the steep part of
+    (the mean SIGNED difference over eighteen coalitions - all ten singletons, eight pairs - within 1 pt),
+    mean |difference| within 2 pt, each within 4 pt (10000 test samples: 1 pt = 100 samples).  One epoch leaves the models in the steep part of
     learning, where fp32 summation order alone moves a single coalition's accuracy by points: the oracle
     against ITSELF, run with 8 vs 3 CPU threads, gives 0.9675 vs 0.9793 for (0, 9), and 0.8766 (8 threads
     here) vs 0.8632 (16 threads on the GPU box) for (2, 7) at signal 0.2 (0.2-0.8 pt apart even at E=2),
@@ -76,7 +76,11 @@ def test_config3_small_coalitions_vs_oracle(mnist10, config3_sweep):
     data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow = [p.train_idx for p in mnist10.partners_list]
     bs = [p.batch_size for p in mnist10.partners_list]
-    coals = [(3,), (6,), (8,), (2, 7), (0, 9), (4, 5)]
+    # every singleton and eight pairs: a single coalition moves by up to ~4 pt with the fp32 summation order
+    # alone (module docstring), so the bias bound needs the larger sample (se of the mean ~0.4 pt here;
+    # profiles/r02_parity_probe_wg8_wg9.txt: mean signed difference -0.44 / +0.15 pt for two summation orders
+    # of conv2's weight gradient, while six coalitions alone gave -0.57 / +1.19 pt)
+    coals = [(p,) for p in range(10)] + [(2, 7), (0, 9), (4, 5), (1, 3), (6, 8), (0, 5), (2, 9), (3, 7)]
     ref = np.array([ocnn.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
     dev = np.array([c.charac_fct_values[k] for k in coals])
     diff = dev - ref
