@@ -1175,6 +1175,8 @@ extern "C" {
 
 int mplc_cifar_stride(void) { return MPLC_CIFAR_STRIDE; }
 
+int mplc_cifar_wgrad_split_samples(void) { return WGS; }
+
 int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
   if (!params || !keys || n_models < 1 || n_models > 65535 || stride != MPLC_CIFAR_STRIDE) return MPLC_E_ARG;
   init_params_kernel<<<dim3(512, n_models), 256, 0, (hipStream_t)stream>>>(params, stride, keys);

@@ -43,6 +43,7 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     # batched CIFAR10 CNN trainer (include/mplc_hip_cifar.h); mplc.cifar re-binds train_step with its struct
     "mplc_cifar_stride": (c_int, []),
+    "mplc_cifar_wgrad_split_samples": (c_int, []),
     "mplc_cifar_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cifar_train_step": (c_int, [c_void_p, c_void_p]),
     "mplc_cifar_eval_workspace_floats": (c_int64, [c_int, c_int]),

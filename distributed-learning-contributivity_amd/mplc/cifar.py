@@ -57,6 +57,8 @@ def _bind():
     lib = _native.lib()
     if lib.mplc_cifar_stride() != STRIDE:
         raise RuntimeError("libmplc_hip.so CIFAR layout mismatch; rebuild")
+    global WG_SAMPLES
+    WG_SAMPLES = int(lib.mplc_cifar_wgrad_split_samples())  # the library's weight-gradient split size
     _BOUND = True
 
 

@@ -60,7 +60,9 @@ extern "C" {
 #define MPLC_CIFAR_DZ1 32768         /* conv1 pre-activation gradient 32x32x32    */
 #define MPLC_CIFAR_WT 64512          /* flipped/transposed W2|W3|W4 for the data gradients */
 #define MPLC_CIFAR_WPART 65664       /* partial gradient row of W1..b4 (= params layout prefix) */
+#ifndef MPLC_CIFAR_WG_SAMPLES
 #define MPLC_CIFAR_WG_SAMPLES 2      /* samples per weight-gradient split (fixed: reproducible sums) */
+#endif
 
 typedef struct {
   /* geometry */
@@ -125,6 +127,9 @@ typedef struct {
 
 /* Parameter row stride in floats (== MPLC_CIFAR_STRIDE). */
 int mplc_cifar_stride(void);
+
+/* Samples per weight-gradient split: mplc_cifar_train_t.wg_splits must be ceil(bmax / this). */
+int mplc_cifar_wgrad_split_samples(void);
 
 /* glorot_uniform kernels / zero biases for n_models rows, keyed per model. */
 int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream);
