@@ -131,10 +131,70 @@ def pmc_traffic(kernel, workload):
     return int(e["traffic_bytes_per_launch"])
 
 
-def dist_init():
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv=None):
+    """`python bench.py --gpus N` without an outer launcher: start N ranks of this same command as child
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, one GPU each) and return the
+    exit status.  The parent never touches the GPU (no torch.cuda call: it only starts and watches the
+    children), so nothing here replaces a process that initialised the device.  Rank 0 prints the JSON line
+    (its stdout is this process's stdout).  When a rank fails, the others are stopped: they would otherwise
+    wait in a collective for the dead one."""
+    import signal
+    import subprocess
+    argv = [os.path.abspath(__file__)] + sys.argv[1:] if argv is None else list(argv)
+    port = _free_port()
+    procs = []
+
+    def forward(signum, frame):  # the parent is stopped (driver time limit, ^C): take the ranks with it
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL if signum != signal.SIGINT else signal.SIGTERM)
+        sys.exit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPLC_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u"] + argv, env=env, start_new_session=True,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"rank {procs.index(p)} exited with {code}: stopping the other ranks")
+                for q in live:
+                    os.killpg(q.pid, signal.SIGTERM)
+        time.sleep(0.2)
+    for q in procs:
+        q.wait()
+    return rc
+
+
+def dist_init(expected=None, use_gpu=True):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if expected is not None and world != expected:
+        raise SystemExit(f"bench.py: --gpus {expected} but the launcher started WORLD_SIZE={world} ranks")
+    if not use_gpu:
+        if world > 1 and not dist.is_initialized():
+            dist.init_process_group("gloo")
+        return int(os.environ.get("RANK", "0")), world, None
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; more ranks than GPUs (a gloo rehearsal of the multi-rank path on a 1-GPU box)
@@ -614,7 +674,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--budget-s", type=float, default=480.0,
                     help="wall-clock budget from process start for the whole run (driver limit: 600 s)")
-    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar"])
+    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar", "dist-check"])
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
     ap.add_argument("--cifar-epochs", type=int, default=1)
@@ -630,7 +690,28 @@ def main():
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()
-    rank, world, _ = dist_init()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # one child process per GPU; this process stays off the GPU
+    rank, world, _ = dist_init(expected=args.gpus, use_gpu=args.leg != "dist-check")
+    if args.leg == "dist-check":
+        # the multi-rank plumbing alone (no GPU): every rank reports (rank, local rank) through one all_gather
+        import torch
+        import torch.distributed as dist
+        mine = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0"))], dtype=torch.int64)
+        got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        if world > 1:
+            dist.all_gather(got, mine)
+        else:
+            got = [mine]
+        if rank == 0:
+            print(json.dumps({"leg": "dist-check", "n_gpus": world, "ranks": [g.tolist() for g in got],
+                              "master": [os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     if args.leg == "shapley":
         out = bench_shapley(args.n, max(args.steps, 5), max(args.warmup, 2), rank, world)
         out.update({"n_gpus": world, "steps": max(args.steps, 5), "warmup": max(args.warmup, 2),

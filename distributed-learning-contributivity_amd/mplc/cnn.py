@@ -258,27 +258,27 @@ class MnistModel:
         import torch
         if not stash:
             return {}
-        cnt = torch.stack([e[0] for e in stash]).to(torch.float64)
-        at = torch.stack([e[1] for e in stash])
-        src = torch.stack([e[2] for e in stash])
-        # distinct coalition rows read per step (rows are < 2^20; steps are offset so rows never collide)
-        steps = torch.arange(src.shape[0], device=src.device, dtype=torch.int64).unsqueeze(1)
-        shared = src >= 0
-        keys = (steps * (1 << 20) + src.to(torch.int64))[shared & (cnt > 0)]
-        n_shared_rows = float(torch.unique(keys).numel())
-        t = at & (ADAM_LAST - 1)
-        last = (at & ADAM_LAST) != 0
-        act = (cnt > 0).to(torch.float64)
+        # one step at a time: the replica count differs between lockstep batches when the memory budget splits
+        # a job into several (the per-step copies then have different lengths)
         w3 = float(FEAT * HID * 4)
-        mom_rd = torch.where(t == 1, 0.0, torch.where(t == 2, 1.0, 2.0)).to(torch.float64)
-        mom_wr = torch.where(last, 0.0, torch.where(t == 1, 1.0, 2.0)).to(torch.float64)
-        own = (~shared).to(torch.float64)  # replicas reading W3 from their own row
-        d1 = act * (w3 * (1.0 + own + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
-        df = act * (w3 * own + cnt * float(FEAT * 4 + HID * 4))
-        shared_w3 = n_shared_rows * w3
-        return {"samples": float(cnt.sum().item()),
-                "dense1_bwd_adam_bytes": float(d1.sum().item()) + shared_w3,
-                "dense_fwd_bytes": float(df.sum().item()) + shared_w3}
+        samples = d1_bytes = df_bytes = 0.0
+        for cnt, at, src in stash:
+            cnt = cnt.to(torch.float64)
+            shared = src >= 0
+            # distinct coalition rows read by this step's first-step replicas
+            n_shared_rows = float(torch.unique(src[shared & (cnt > 0)]).numel())
+            t = at & (ADAM_LAST - 1)
+            last = (at & ADAM_LAST) != 0
+            act = (cnt > 0).to(torch.float64)
+            mom_rd = torch.where(t == 1, 0.0, torch.where(t == 2, 1.0, 2.0)).to(torch.float64)
+            mom_wr = torch.where(last, 0.0, torch.where(t == 1, 1.0, 2.0)).to(torch.float64)
+            own = (~shared).to(torch.float64)  # replicas reading W3 from their own row
+            d1 = act * (w3 * (1.0 + own + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
+            df = act * (w3 * own + cnt * float(FEAT * 4 + HID * 4))
+            samples += float(cnt.sum().item())
+            d1_bytes += float(d1.sum().item()) + n_shared_rows * w3
+            df_bytes += float(df.sum().item()) + n_shared_rows * w3
+        return {"samples": samples, "dense1_bwd_adam_bytes": d1_bytes, "dense_fwd_bytes": df_bytes}
 
     def evaluate(self, eng, sel, x, y):
         """(correct counts, mean CE) of the C models in `sel` [C][STRIDE] on (x, y)."""
@@ -430,8 +430,14 @@ class TrainBatch:
                 ww, scl = aggregation_weights([sizes[p] for p in self.coalitions[ci]], self.eng.aggregation)
                 w.extend(ww)
                 sc.append(scl)
+            # the broadcast may skip W3 / W5 only if every member trains in every round: a round's first step
+            # is what reloads them from the coalition row, and a partner with an empty minibatch (fewer rows
+            # than minibatch_count) has no step in that round, yet enters the average with the round's global
+            # model (the reference's fresh model from the global weights, mplc/multi_partner_learning.py:319)
+            full_bcast = any(self.eng.bounds[p][m + 1] == self.eng.bounds[p][m]
+                             for ci in run for p in self.coalitions[ci] for m in range(self.eng.minibatch_count))
             args.append((self.coal_first[run[0]], run[0], len(run), f, torch.tensor(w, dtype=torch.float64, device=self.dev),
-                         torch.tensor(sc, dtype=torch.float64, device=self.dev)))
+                         torch.tensor(sc, dtype=torch.float64, device=self.dev), full_bcast))
         return args
 
     def step(self, s):
@@ -457,10 +463,11 @@ class TrainBatch:
         S, NP = self.model.STRIDE, self.model.NPARAM
         aggregate_now = (not self.seq_mode or self.approach == "seqavg"
                          or (self.approach == "seq-with-final-agg" and epoch_end))
-        for (r0, c0, nc, first, w, sc) in self.run_args:
+        for (r0, c0, nc, first, w, sc, full_bcast) in self.run_args:
             if aggregate_now:
                 x = self.params[r0:] if not self.seq_mode else self.snap[self.snap_row(c0):]
-                skip = None if self.seq_mode else getattr(self.model, "BCAST_SKIP", None)
+                skip = None if (self.seq_mode or full_bcast or not self.eng.bcast_skip) else \
+                    getattr(self.model, "BCAST_SKIP", None)
                 if skip is not None:  # the next round's first step reads this range from glob
                     _native.check(self.lib.mplc_fedavg_aggregate_bcast_skip(
                         _native.ptr(x), S, _native.ptr(first), _native.ptr(w), _native.ptr(sc), nc, NP,

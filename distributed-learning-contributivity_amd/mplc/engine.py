@@ -89,10 +89,16 @@ class CoalitionEngine:
             # memory the caching allocator holds but no tensor uses (an earlier engine's lockstep batches) is
             # as good as free for this engine's batches; mem_get_info does not count it
             free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-            memory_budget_bytes = max(int(free * 0.8) - self.eval_budget_bytes, 1 << 30)
+            memory_budget_bytes = int(free * 0.8) - self.eval_budget_bytes
+            if memory_budget_bytes < (256 << 20):
+                raise RuntimeError(f"not enough free device memory for the coalition engine: {free >> 20} MiB free, "
+                                   f"{self.eval_budget_bytes >> 20} MiB reserved for evaluation")
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): in-stream HIP events around the step kernels
+        # FedAvg rounds leave the large dense layer out of the broadcast (the next round's first step reads it
+        # from the coalition row); False broadcasts every layer (the plain copy-back, for A/B tests)
+        self.bcast_skip = True
         self.stats = {"coalitions": 0, "batches": 0, "replicas": 0, "samples": 0}
 
     # --------------------------------------------------------------------------------------------

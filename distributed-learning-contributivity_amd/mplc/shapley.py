@@ -76,11 +76,39 @@ def shard_range(n, rank, world_size):
     return b0 * SPAN, b1 * SPAN
 
 
+def sharded_shapley(V, n, rank, world_size):
+    """SV of a full bitmask table that every rank holds (the all-reduced v(S) of the engine's sharded
+    evaluation): each rank reduces its block-aligned mask range [shard_range) once, the 2(n+1) partial sums
+    are all_reduced (RCCL on the GPUs; through host memory for a gloo rehearsal), and every rank finalizes the
+    same SV.  The sums are linear in V, so the result equals the one-pass kernel's to rounding
+    (1e-12 relative, tests/test_shapley_gpu.py)."""
+    import torch.distributed as dist
+    torch = _torch()
+    begin, end = shard_range(n, rank, world_size)
+    agg = ShapleyAggregator(n, device=V.device, count=max(end - begin, SPAN))
+    if end > begin:
+        part = agg.partial(V[begin:end], begin)
+    else:
+        part = agg.partial_buf.zero_()
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(part)
+    else:
+        host = part.cpu()
+        dist.all_reduce(host)
+        part.copy_(host)
+    return agg.finalize(part).cpu().numpy()
+
+
 def shapley_from_table(V, n):
-    """SV (numpy float64, length n) of a bitmask-ordered table given as numpy array or device tensor."""
+    """SV (numpy float64, length n) of a bitmask-ordered table given as numpy array or device tensor.  Under
+    torch.distributed with n >= 16 the table is reduced range-sharded across the ranks (sharded_shapley)."""
+    from .parallel import world
     torch = _torch()
     if isinstance(V, np.ndarray):
         V = torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)).cuda()
+    rank, ws = world()
+    if ws > 1 and n >= 16:
+        return sharded_shapley(V, n, rank, ws)
     agg = ShapleyAggregator(n, device=V.device)
     return agg.run(V).cpu().numpy()
 

@@ -201,16 +201,28 @@ def conv1_relu_flip_bound(p, x, y, rel_tau=1e-6):
 class KerasAdam:
     """Keras 2.3.1 Adam (keras/optimizers.py get_updates), float32."""
 
-    def __init__(self, params, lr=0.001, beta_1=0.9, beta_2=0.999, eps=1e-7):
+    def __init__(self, params, lr=0.001, beta_1=0.9, beta_2=0.999, eps=1e-7, precise=False):
+        """precise=True: the same fp32 constants, every derived scalar kept in fp64 (with fp64 params: the
+        high-precision restatement of the same update)."""
         torch = _torch()
         self.lr, self.b1, self.b2, self.eps = (np.float32(lr), np.float32(beta_1), np.float32(beta_2), np.float32(eps))
         self.m = {k: torch.zeros_like(v) for k, v in params.items()}
         self.v = {k: torch.zeros_like(v) for k, v in params.items()}
         self.t = 0
+        self.precise = precise
 
     def step(self, params, grads):
         torch = _torch()
         self.t += 1
+        if self.precise:
+            b1, b2 = float(self.b1), float(self.b2)
+            lr_t = float(self.lr) * np.sqrt(1.0 - b2 ** self.t) / (1.0 - b1 ** self.t)
+            for k in params:
+                g = grads[k]
+                self.m[k] = b1 * self.m[k] + (1.0 - b1) * g
+                self.v[k] = b2 * self.v[k] + (1.0 - b2) * (g * g)
+                params[k] = params[k] - lr_t * self.m[k] / (torch.sqrt(self.v[k]) + float(self.eps))
+            return
         t = np.float32(self.t)
         lr_t = self.lr * (np.sqrt(np.float32(1) - np.power(self.b2, t)) / (np.float32(1) - np.power(self.b1, t)))
         lr_t = float(np.float32(lr_t))
@@ -249,14 +261,40 @@ class Data:
         self.x_test, self.y_test = img(x_test), lab(y_test)
 
 
-def average_models(glob, models, w):
-    """np.average(..., axis=0, weights=w) per layer in float64 -> float32 (mplc/mpl_utils.py:90-102)."""
+def average_models(glob, models, w, keep_f64=False):
+    """np.average(..., axis=0, weights=w) per layer in float64 -> float32 (mplc/mpl_utils.py:90-102);
+    keep_f64: the float64 average itself (the fp64 restatement)."""
     torch = _torch()
     new = {}
     for k in glob:
         stack = np.array([pm[k].numpy() for pm in models])
-        new[k] = torch.from_numpy(np.average(stack, axis=0, weights=w).astype(np.float32))
+        avg = np.average(stack, axis=0, weights=w)
+        new[k] = torch.from_numpy(avg if keep_f64 else avg.astype(np.float32))
     return new
+
+
+def fedavg_round(data, partner_rows, batch_sizes, coalition, glob, seed=0, M=20, e=0, m=0, precise=False):
+    """One FedAvg round (epoch e, minibatch m; mplc/multi_partner_learning.py:301-334) from the global model
+    `glob` (dict of tensors): every partner a fresh Keras Adam over its round rows at its batch size, then the
+    data-volume average (mplc/mpl_utils.py:90-115).  precise=True runs the same schedule with every tensor
+    operation in float64 (gradients, Adam, the average kept in fp64): the high-precision reference of the same
+    algorithm against which fp32 implementations' rounding is measured."""
+    torch = _torch()
+    coalition = tuple(sorted(coalition))
+    mask = sum(1 << p for p in coalition)
+    dt = torch.float64 if precise else torch.float32
+    sizes = [len(partner_rows[p]) for p in coalition]
+    w = np.asarray(sizes) / np.sum(sizes)
+    models = []
+    for p_id in coalition:
+        key = shuffle_key(seed, mask, p_id)
+        params = {k: v.to(dt).clone() for k, v in glob.items()}
+        opt = KerasAdam(params, precise=precise)
+        for rows in fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m):
+            g, _ = gradients(params, data.x_train[rows], data.y_train[rows], dtype=dt if precise else None)
+            opt.step(params, g)
+        models.append(params)
+    return average_models(glob, models, w, keep_f64=precise)
 
 
 class _FitLog:

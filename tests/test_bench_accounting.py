@@ -65,3 +65,21 @@ def test_shared_coalition_rows_count_once():
     # W3 write + g write per replica, two distinct coalition rows read
     assert u["dense1_bwd_adam_bytes"] == 4 * 2 * W3 + 91 * per_sample_bwd + 2 * W3
     assert u["dense_fwd_bytes"] == 91 * (9216 * 4 + 128 * 4) + 2 * W3
+
+
+def test_steps_of_batches_with_different_replica_counts():
+    """A job split into several lockstep batches (memory budget) stashes per-step schedules of different
+    lengths: the totals are the sums of the per-step counts (torch.stack raised here)."""
+    L = cnn.ADAM_LAST
+    a = (torch.tensor([27, 27, 0], dtype=torch.int32), torch.tensor([1, 2, 0], dtype=torch.int32),
+         torch.tensor([3, -1, -1], dtype=torch.int32))
+    b = (torch.tensor([11, 27, 27, 5, 9], dtype=torch.int32), torch.tensor([3, 4 | L, 1, 1, 2], dtype=torch.int32),
+         torch.tensor([-1, -1, 0, 0, -1], dtype=torch.int32))
+    both = cnn.MnistModel.algorithmic_units([a, b])
+    ua, ub = cnn.MnistModel.algorithmic_units([a]), cnn.MnistModel.algorithmic_units([b])
+    for k in ("samples", "dense1_bwd_adam_bytes", "dense_fwd_bytes"):
+        assert both[k] == ua[k] + ub[k]
+    assert both["samples"] == 27 + 27 + 11 + 27 + 27 + 5 + 9
+    # batch b's step: coalition row 0 read once by its two first-step replicas
+    per_sample_fwd = 9216 * 4 + 128 * 4
+    assert ub["dense_fwd_bytes"] == 3 * W3 + W3 + 79 * per_sample_fwd  # three own rows + the shared one

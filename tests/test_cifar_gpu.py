@@ -215,3 +215,18 @@ def test_contributivity_tmcs_on_cifar():
     assert c.name == "TMC Shapley"
     assert np.all(np.isfinite(c.contributivity_scores))
     assert c.first_charac_fct_calls_count >= 1
+
+
+def test_empty_minibatch_partner_restarts_from_global_model():
+    """As tests/test_cnn_gpu.py for the CIFAR10 trainer's W5-broadcast skip."""
+    from mplc.engine import CoalitionEngine
+    sc = make_scenario(partners=2, amounts=(0.01, 0.99), M=20, G=2, E=1)
+    assert len(sc.partners_list[0].train_idx) < 20
+    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    coals = [(0, 1), (1,)]
+    skip = eng.evaluate(coals, return_models=True, return_details=True)
+    eng.bcast_skip = False
+    full = eng.evaluate(coals, return_models=True, return_details=True)
+    assert np.array_equal(skip["scores"], full["scores"])
+    for a, b in zip(skip["models"][0], full["models"][0]):
+        assert np.array_equal(a, b)

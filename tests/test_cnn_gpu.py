@@ -352,3 +352,64 @@ def test_scenario_run_saves_final_model(tmp_path):
                      sc.dataset.x_test, sc.dataset.y_test)
     _, acc = ocnn.evaluate(ocnn.unpack(row), data.x_test, data.y_test)
     assert abs(acc - sc.mpl.history.score) <= 1 / len(data.y_test) + 1e-12, (acc, sc.mpl.history.score)
+
+
+def test_empty_minibatch_partner_restarts_from_global_model():
+    """a FedAvg partner with fewer rows than minibatch_count has empty minibatches; in those rounds
+    it trains nothing and enters the average with the round's global model (the reference builds it fresh
+    from the global weights, mplc/multi_partner_learning.py:319).  The W3-broadcast skip must not leave it a
+    stale W3: values equal the plain copy-back path bit for bit, with and without other coalitions in the
+    batch, and follow the oracle."""
+    from mplc.engine import CoalitionEngine
+    sc = make_scenario(partners=2, amounts=(0.01, 0.99), M=20, G=2, E=1)
+    prow, bs = rows(sc)
+    assert len(prow[0]) < 20  # empty splits for partner 0
+    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    coals = [(0, 1), (0,), (1,)]
+    skip = eng.evaluate(coals, return_models=True, return_details=True)
+    eng.bcast_skip = False
+    full = eng.evaluate(coals, return_models=True, return_details=True)
+    assert np.array_equal(skip["scores"], full["scores"])
+    for a, b in zip(skip["models"][0], full["models"][0]):
+        assert np.array_equal(a, b)
+    ds = sc.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    ref, _ = ocnn.coalition_value(data, prow, bs, (0, 1), seed=eng.seed, epochs=1, M=20)
+    assert abs(skip["scores"][0] - ref) <= 0.03, (skip["scores"][0], ref)
+
+
+def test_early_stopping_epoch_pinned_to_oracle():
+    """The stopping EPOCH against the oracle, on a case whose val-loss curve is steep at the stop: 60 % of the
+    digits training labels randomised and G=32 (64 Keras steps per epoch), so the models overfit fast and
+    the val loss climbs by 0.05-0.5 per epoch where the rules fire (MultiPartnerLearning.early_stop,
+    mplc/multi_partner_learning.py:177-193; Keras EarlyStopping(patience=10) for singletons, :247-260).
+    The oracle's own thread-count spread on this case (8 vs 3 CPU threads, measured in the build container):
+    (0,) stops at 12 vs 12, (0, 1) at 13 vs 13 - pinned exactly; (1,) at 14 vs 13 (its val-loss minimum is a
+    near-tie, 1.980 vs 1.981) - pinned to +-1 epoch."""
+    from mplc.dataset import ArrayDataset, digits_as_mnist
+    from mplc.engine import CoalitionEngine
+    from mplc.scenario import Scenario
+    x, y = digits_as_mnist()
+    y = np.array(y).copy()
+    y = np.argmax(y, 1) if y.ndim == 2 else y
+    rng = np.random.default_rng(0)
+    flip = rng.random(1500) < 0.6
+    y[np.arange(1500)[flip]] = rng.integers(0, 10, size=int(flip.sum()))
+    ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:])
+    E = 30
+    sc = Scenario(2, [0.3, 0.7], dataset=ds, minibatch_count=2, gradient_updates_per_pass_count=32, epoch_count=E,
+                  is_early_stopping=True).provision()
+    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    coals = [(0,), (1,), (0, 1)]
+    res = eng.evaluate(coals, return_details=True)
+    d = sc.dataset
+    data = ocnn.Data(d.x_train, d.y_train, d.x_val, d.y_val, d.x_test, d.y_test)
+    prow, bs = rows(sc)
+    tol = {(0,): 0, (1,): 1, (0, 1): 0}
+    for i, c in enumerate(coals):
+        ref_trace = []
+        _, ref_ep = ocnn.coalition_value(data, prow, bs, c, seed=eng.seed, epochs=E, M=2, early_stopping=True,
+                                         es_trace=ref_trace)
+        assert ref_ep < E
+        assert abs(int(res["epochs_done"][i]) - ref_ep) <= tol[c], (c, res["epochs_done"][i], ref_ep,
+                                                                    res["es_val_loss"][i], ref_trace)

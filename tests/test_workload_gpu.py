@@ -158,3 +158,151 @@ def test_config4_coalitions_vs_oracle(cifar20, config4_tmcs):
     ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
     diff = np.abs(dev - ref)
     assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
+
+
+# ------------------------------------------------------------------------------------------------
+# config #4, the SMCS half: Stratified MC (mplc/contributivity.py:727-819) and WR_SMC (:823-938) on the
+# HIP engine.  20 partners would need ~17k coalition fits for SMCS's stopping rule (every stratum of every
+# player > 20 samples); 10 partners ([0.1] * 10) keep the test near a minute, as bench.py --method SMCS
+# --cifar-partners 10 does.
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cifar10p():
+    from mplc.dataset import Cifar10
+    from mplc.scenario import Scenario
+    sc = Scenario(10, [0.1] * 10, dataset=Cifar10(synthetic=True, signal=0.4), minibatch_count=20,
+                  gradient_updates_per_pass_count=8, epoch_count=1, is_early_stopping=False)
+    return sc.provision()
+
+
+@pytest.fixture(scope="module")
+def config4_smc(cifar10p):
+    """SMCS then WR_SMC, numpy seed 0 each, on the engine (speculative planning on); the coalition cache is
+    the scenario's, so WR_SMC reuses SMCS's trained coalitions."""
+    from mplc.contributivity import Contributivity
+    out = {}
+    for method in ("SMCS", "WR_SMC"):
+        np.random.seed(0)
+        c = Contributivity(scenario=cifar10p)
+        c.compute_contributivity(method)
+        out[method] = c
+    return out
+
+
+@pytest.mark.parametrize("method,name", [("SMCS", "Stratified MC Shapley"), ("WR_SMC", "WR_SMC Shapley")])
+def test_config4_smc_batched_equals_sequential_reference_loop(cifar10p, config4_smc, method, name, monkeypatch):
+    """The reference's sequential loop (one fit per coalition through the plug-in protocol, no planning), fed
+    the v(S) values the engine trained, reproduces scores, std, call count and memo order bit for bit."""
+    import mplc.multi_partner_learning as mpl_mod
+    from mplc.contributivity import Contributivity
+    c = config4_smc[method]
+    table = dict(cifar10p.coalition_values)
+    calls = []
+
+    class TableMPL:
+        def __init__(self, scenario, partners_list=None, partner=None, **kw):
+            if partner is not None:
+                partners_list = [partner]
+            self.ids = tuple(sorted(int(p.id) for p in partners_list))
+            self.history = types.SimpleNamespace(score=None)
+
+        def fit(self):
+            calls.append(self.ids)
+            self.history.score = table[self.ids]
+
+    monkeypatch.setattr(mpl_mod, "SinglePartnerLearning", TableMPL)
+    plain = types.SimpleNamespace(partners_list=cifar10p.partners_list, multi_partner_learning_approach=TableMPL)
+    np.random.seed(0)
+    ref = Contributivity(scenario=plain)
+    ref.compute_contributivity(method)
+    assert ref.name == c.name == name
+    assert np.array_equal(ref.contributivity_scores, c.contributivity_scores)
+    assert np.array_equal(ref.scores_std, c.scores_std)
+    assert ref.first_charac_fct_calls_count == c.first_charac_fct_calls_count == len(calls)
+    assert list(ref.charac_fct_values) == list(c.charac_fct_values)
+    assert [ref.increments_values[i] == c.increments_values[i] for i in range(10)] == [True] * 10
+    assert c.first_charac_fct_calls_count > 200 and np.all(np.isfinite(c.contributivity_scores))
+
+
+def test_config4_smc_values_are_engine_values_and_vs_oracle(cifar10p, config4_smc):
+    """Every memo entry is the engine's v(S) for that coalition (re-evaluated alone: bit-identical), and two
+    coalitions the SMCS run drew follow oracle/cifar_cnn.py (sequential, same keys and schedule)."""
+    from oracle import cifar_cnn as occ
+    c = config4_smc["SMCS"]
+    eng = cifar10p.engine
+    keys = [k for k in c.charac_fct_values if len(k) in (1, 2)]
+    assert keys, "SMCS drew no singleton or pair"
+    picks = [keys[0], keys[-1]] if len(keys) > 1 else keys
+    dev = eng.evaluate(picks)
+    assert [float(v) for v in dev] == [c.charac_fct_values[k] for k in picks]
+    ds = cifar10p.dataset
+    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in cifar10p.partners_list]
+    bs = [p.batch_size for p in cifar10p.partners_list]
+    ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in picks])
+    diff = np.abs(np.asarray(dev) - ref)
+    assert np.max(diff) <= 0.03, (picks, dev, ref)
+
+
+# ------------------------------------------------------------------------------------------------
+# config #3 numerics, deterministic: one full FedAvg round, device vs the fp64 restatement
+# ------------------------------------------------------------------------------------------------
+def test_config3_round_trajectory_vs_fp64(mnist10):
+    """One FedAvg round of config #3's shape (3 partners x 9 Keras-Adam steps at bs 27 on their 219-row
+    minibatch, then the data-volume average) on the Winograd kernels, against the oracle's schedule run in
+    fp64 (oracle/cnn.py fedavg_round(precise=True)) from the same keyed initial model.  Per tensor, the
+    device's error on the round's update, ||dev - ref64|| / ||ref64 - start||, must be <= 4x the oracle's own
+    fp32 run's error on the same round: this pins the kernels' rounding (Winograd transforms, MFMA
+    accumulation order, the fused Adam) with no accuracy noise in the way."""
+    import torch
+    from oracle import cnn as ocnn
+    from mplc.engine import CoalitionEngine
+    eng = CoalitionEngine.for_scenario(mnist10, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
+    coal = (0, 3, 7)
+    st = eng.trainer.prepare([coal], 1)
+    assert st.round_len == 9 and all(mnist10.partners_list[p].batch_size == 27 for p in coal)
+    start = st.glob[0].cpu().numpy().copy()
+    for s in range(st.round_len):
+        st.step(s)
+    st.aggregate()
+    torch.cuda.synchronize()
+    dev = st.glob[0].cpu().numpy()
+    ds = mnist10.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in mnist10.partners_list]
+    bs = [p.batch_size for p in mnist10.partners_list]
+    glob = ocnn.unpack(start)
+    assert np.array_equal(start, ocnn.init_params(ocnn.init_key(eng.seed, sum(1 << p for p in coal))))
+    g32 = ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=20)
+    g64 = ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=20, precise=True)
+    report, bad = [], []
+    for name, (off, shape) in ocnn.OFF.items():
+        n = int(np.prod(shape))
+        ref = g64[name].numpy().reshape(-1)
+        upd = np.linalg.norm(ref - start[off:off + n].astype(np.float64))
+        err_dev = np.linalg.norm(dev[off:off + n].astype(np.float64) - ref) / upd
+        err_cpu = np.linalg.norm(g32[name].numpy().reshape(-1).astype(np.float64) - ref) / upd
+        report.append((name, float(err_dev), float(err_cpu)))
+        if not err_dev <= 4 * err_cpu:
+            bad.append(report[-1])
+    print(report)
+    assert not bad, (bad, report)
+
+
+def test_config3_e2_accuracies_vs_oracle(mnist10):
+    """v(S) at E=2 (the bench's config #3 setting; the oracle's own run-to-run spread is 0.2-0.8 pt there) on
+    eight coalitions fixed before looking at results: mean signed difference <= 1 pt, each <= 2 pt."""
+    from oracle import cnn as ocnn
+    from mplc.engine import CoalitionEngine
+    eng = CoalitionEngine.for_scenario(mnist10, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
+    coals = [(0,), (4,), (9,), (1, 2), (3, 8), (5, 7), (0, 6, 9), (1, 4, 5, 8)]
+    dev = eng.evaluate(coals, epoch_count=2)
+    ds = mnist10.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in mnist10.partners_list]
+    bs = [p.batch_size for p in mnist10.partners_list]
+    ref = np.array([ocnn.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=2, M=20)[0] for k in coals])
+    diff = dev - ref
+    print(list(zip(coals, dev.tolist(), ref.tolist())))
+    assert abs(np.mean(diff)) <= 0.01, (dev, ref)
+    assert np.max(np.abs(diff)) <= 0.02, (dev, ref)
