@@ -238,11 +238,12 @@ def sum_over_ranks(x, world):
     return float(t.item())
 
 
-def run_budgeted(warm_step, timed_step, args, world, reserve_s, what):
-    """Warm-up (at most one step of `warm_step`) + timed steps of `timed_step` under the wall-clock budget.
-    Returns (steps run, warm-up steps run, wall seconds of the timed region (max over ranks), the last step's
-    result).  Every rank takes the same decisions: they are made from max-over-ranks times."""
-    warm = min(args.warmup, 1)
+def run_budgeted(warm_step, timed_step, args, world, reserve_s, what, max_steps=None, warmup=None):
+    """Warm-up (at most one step of `warm_step`) + timed steps of `timed_step(i, planned)` under the wall-clock
+    budget.  Returns (steps run, warm-up steps run, wall seconds of the timed region (max over ranks), the last
+    step's result, per-step seconds).  Every rank takes the same decisions: they are made from max-over-ranks
+    times."""
+    warm = min(args.warmup if warmup is None else warmup, 1)
     t_step = 0.0
     for _ in range(warm):
         t = time.perf_counter()
@@ -252,19 +253,22 @@ def run_budgeted(warm_step, timed_step, args, world, reserve_s, what):
         log(f"{what}: warm-up step {t_step:.1f}s")
     elapsed = max_over_ranks(time.perf_counter() - T_PROC0, world)
     left = args.budget_s - elapsed - reserve_s
-    steps = args.steps
+    steps = args.steps if max_steps is None else min(args.steps, max_steps)
+    requested = steps
     if t_step > 0:
-        steps = max(1, min(args.steps, int(left // (t_step * 1.03))))
-    log(f"{what}: timing {steps} of {args.steps} requested steps ({left:.0f}s left for them)")
+        steps = max(1, min(steps, int(left // (t_step * 1.03))))
+    log(f"{what}: timing {steps} of {requested} requested steps ({left:.0f}s left for them)")
     barrier(world)
     t0 = time.perf_counter()
     res = None
     done = 0
+    per_step = []
     for i in range(steps):
         ts = time.perf_counter()
-        res = timed_step()
+        res = timed_step(i, steps)
         done += 1
-        log(f"{what}: step {i + 1}/{steps} {time.perf_counter() - ts:.1f}s")
+        per_step.append(time.perf_counter() - ts)
+        log(f"{what}: step {i + 1}/{steps} {per_step[-1]:.1f}s")
         if t_step == 0 and done < steps:
             # no warm-up estimate: stop early rather than overrun (decided on rank-0's clock, broadcast by max)
             over = (time.perf_counter() - T_PROC0) + (time.perf_counter() - ts) + reserve_s > args.budget_s
@@ -272,7 +276,8 @@ def run_budgeted(warm_step, timed_step, args, world, reserve_s, what):
                 break
     barrier(world)
     wall = max_over_ranks(time.perf_counter() - t0, world)
-    return done, warm, wall, res
+    per_step = [max_over_ranks(t, world) for t in per_step]
+    return done, warm, wall, res, per_step
 
 
 # --------------------------------------------------------------------------------------------------
@@ -488,22 +493,29 @@ def bench_train(args, rank, world):
 
     timer = KernelTimer("all", TRAIN_KERNELS, stash=True)
     reps0 = [None]
+    n_on = [0]
 
-    def timed_step():
-        if eng.profiler is None and reps0[0] is None:  # the timed region starts: attach the in-stream timer
-            eng.profiler = None if args.no_kernel_timer else timer
+    def timed_step(i, planned):
+        # the in-stream kernel timer (an event pair around every launch) runs on the first half of the timed
+        # steps only; the second half runs without events, so the line shows what the timer itself costs
+        if reps0[0] is None:
             reps0[0] = eng.stats["replicas"]
+        on = not args.no_kernel_timer and (i < max(1, (planned + 1) // 2))
+        eng.profiler = timer if on else None
+        n_on[0] += int(on)
         return one_step()
 
-    # reserve: the N=28 aggregation leg (~10 s with its table) and, at N=1, the bounded CPU baseline (~40 s)
-    reserve = (0 if args.no_shapley_agg else 15) + (45 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
-    steps, warm, wall, c = run_budgeted(one_step, timed_step, args, world, reserve, "train")
+    # reserve: the N=28 aggregation leg (~10 s with its table), at N=1 the bounded CPU baselines (~40 s + ~15 s)
+    # and the config #4 sub-leg (one CIFAR10 TMCS run: ~110 s on one GPU)
+    reserve = ((0 if args.no_shapley_agg else 15) + (45 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
+               + (0 if args.no_cifar else CIFAR_SUBLEG_S / world + 25 + (20 if world == 1 else 0)))
+    steps, warm, wall, c, per_step = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
     timer.stash = []
     kernels = kernel_table(timer, units)
     local_reps = eng.stats["replicas"] - reps0[0]
-    samples = units.get("samples", 0.0)
+    samples = units.get("samples", 0.0) / max(1, n_on[0]) * steps  # the stash covers the timer-on steps
     ms_per_step = wall * 1000 / steps
     total_train_samples = sum_over_ranks(samples, world)
     # the roofline kernel: the one with the largest share of the step's kernel time
@@ -511,6 +523,11 @@ def bench_train(args, rank, world):
         kernels = {}
         samples = steps * args.epochs * sum(eng.partner_sizes) * (2 ** (n - 1)) / world
         total_train_samples = sum_over_ranks(samples, world)
+    on_ms, off_ms = per_step[:n_on[0]], per_step[n_on[0]:]
+    timer_note = {"steps_with_kernel_timer": n_on[0],
+                  "ms_per_step_timer_on": round(1000 * sum(on_ms) / len(on_ms), 1) if on_ms else None,
+                  "ms_per_step_timer_off": round(1000 * sum(off_ms) / len(off_ms), 1) if off_ms else None,
+                  "note": "value covers every timed step; the kernels table and roofline come from the timer-on steps"}
     dom = max((k for k in kernels if "frac" in kernels[k]), key=lambda k: kernels[k]["ms_total"], default=None)
     kd = kernels.get(dom, {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
                            "launches": 0, "ms_avg": None, "time_share": None, "units_per_launch": None})
@@ -546,6 +563,7 @@ def bench_train(args, rank, world):
                                                           "the whole steps that fit the wall-clock budget"},
         "roofline": roof,
         "kernels": kernels,
+        "kernel_timer": timer_note,
         "shapley_values": [round(float(v), 6) for v in c.contributivity_scores],
         # coalition evaluations as the reference counts them, and the realised epochs (fixed E,
         # early stopping off, so every coalition trains exactly E epochs)
@@ -599,7 +617,13 @@ def cpu_baseline_cifar(sc, coalitions, epochs, M):
                        f"linearly in |S|: {total:.0f}s")}
 
 
-def bench_cifar(args, rank, world):
+CIFAR_SUBLEG_S = 115.0  # one config #4 TMCS run on one MI355X (round-2 measurement: 107 s)
+
+
+def bench_cifar(args, rank, world, sub=False):
+    """Config #4 (CIFAR10 TMCS/SMCS).  sub=True: the sub-leg of the default bench line - exactly one timed
+    TMCS run, no warm-up step (the code object is loaded by eng.warmup(); each lockstep batch allocates its
+    own buffers anyway)."""
     import numpy as np
     from mplc.cifar import FLOP_PER_SAMPLE
     from mplc.contributivity import Contributivity
@@ -624,14 +648,17 @@ def bench_cifar(args, rank, world):
         c.compute_contributivity(args.method)
         return c
 
-    def timed_step():
+    def timed_step(i, planned):
         if eng.profiler is None:
             eng.profiler = timer
             s0[0] = eng.stats["samples"]
         return one_step()
 
-    reserve = (60 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
-    steps, warm, wall, c = run_budgeted(one_step, timed_step, args, world, reserve, "cifar")
+    if sub:
+        steps, warm, wall, c, _ = run_budgeted(one_step, timed_step, args, world, 0, "cifar", max_steps=1, warmup=0)
+    else:
+        reserve = (60 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
+        steps, warm, wall, c, _ = run_budgeted(one_step, timed_step, args, world, reserve, "cifar")
     eng.profiler = None
     kern_ms = timer.total_ms()
     launches = timer.launches()
@@ -687,6 +714,7 @@ def main():
     ap.add_argument("--n", type=int, default=28)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shapley-agg", action="store_true")
+    ap.add_argument("--no-cifar", action="store_true", help="leave out the config #4 sub-leg of the default line")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()
@@ -743,6 +771,18 @@ def main():
             # the kernel-trace average of shapley_block_kernel must stay the N=28 launch
             out["shapley_agg"] = agg
             log(f"shapley_agg N={args.n}: {agg['value']} GB/s")
+        if not args.no_cifar:
+            # BASELINE config #4 in the same line: one CIFAR10 TMCS run (20 partners), its own roofline and CPU
+            # baseline; the MNIST lockstep buffers are returned first
+            sc.engine.release()
+            c4, c4_sc, c4_coals = bench_cifar(args, rank, world, sub=True)
+            if rank == 0:
+                c4["cpu_baseline"] = (cpu_baseline_cifar(c4_sc, c4_coals, args.cifar_epochs, 20)
+                                      if (world == 1 and not args.no_cpu_baseline) else None)
+            for k in ("n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype", "budget", "warmup"):
+                c4.pop(k, None)
+            out["config4"] = c4
+            log(f"config #4 sub-leg: {c4['value']} evals/s")
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
                                    if (world == 1 and not args.no_cpu_baseline) else None)

@@ -49,35 +49,57 @@ def _compile(src, obj, verbose):
     return obj
 
 
-def build(verbose=False, force=False, jobs=8):
-    os.makedirs(BUILD, exist_ok=True)
+# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build: the C ABI's argument validation,
+# workspace sizing and launch set-up run instrumented; device code is compiled as usual (GPU sanitizers are not
+# available on the pool).  Each -fsanitize= sits directly after -Xarch_host so that it applies to the host pass
+# only.  Output: build/asan/libmplc_hip.so (never the product library).
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+SAN_BUILD = os.path.join(BUILD, "asan")
+SAN_LIB = os.path.join(SAN_BUILD, "libmplc_hip.so")
+
+
+def build(verbose=False, force=False, jobs=8, sanitize=False):
+    global CFLAGS
+    build_dir = SAN_BUILD if sanitize else BUILD
+    lib = SAN_LIB if sanitize else LIB
+    os.makedirs(build_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     if not srcs:
         raise RuntimeError("no HIP sources found")
+    base = CFLAGS
+    if sanitize:
+        CFLAGS = CFLAGS + SAN_FLAGS
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(BUILD, os.path.basename(s)[:-4] + ".o")
+        o = os.path.join(build_dir, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
         if force or _stale(o, _deps(s)):
             todo.append((s, o))
-    if todo:
-        with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
-            list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
-    if force or todo or _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+    try:
+        if todo:
+            with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+                list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
+    finally:
+        CFLAGS = base
+    if force or todo or _stale(lib, objs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs
+        if sanitize:
+            cmd += ["-fsanitize=address", "-fsanitize=undefined", "-shared-libsan"]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="host ASan/UBSan build into build/asan/")
     a = ap.parse_args()
-    print(build(verbose=a.verbose, force=a.force))
+    print(build(verbose=a.verbose, force=a.force, sanitize=a.sanitize))
     sys.exit(0)

@@ -7,7 +7,9 @@ import ctypes
 import os
 import threading
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmplc_hip.so")
+# MPLC_LIB_PATH: another build of the same library (tests/test_native_sanitize.py loads the host-ASan build)
+_LIB_PATH = os.environ.get("MPLC_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                            "libmplc_hip.so")
 _lock = threading.Lock()
 _lib = None
 

@@ -151,22 +151,51 @@ def gradients(p, x, y, masks, dtype=None):
 class KerasRMSprop:
     """Keras 2.3.1 RMSprop (keras/optimizers.py get_updates), float32."""
 
-    def __init__(self, params, lr=1e-4, rho=0.9, eps=1e-7, decay=1e-6):
+    def __init__(self, params, lr=1e-4, rho=0.9, eps=1e-7, decay=1e-6, precise=False):
+        """precise=True: the same fp32 constants, the decayed learning rate kept in fp64 (with fp64 params:
+        the high-precision restatement of the same update)."""
         torch = _torch()
         self.lr, self.rho, self.eps, self.decay = np.float32(lr), np.float32(rho), np.float32(eps), np.float32(decay)
         self.omr = np.float32(1.0 - rho)  # (1. - self.rho) on the Python double, then fp32
         self.a = {k: torch.zeros_like(v) for k, v in params.items()}
         self.iterations = 0
+        self.precise = precise
 
     def step(self, params, grads):
         torch = _torch()
         it = np.float32(self.iterations)
-        lr_t = float(self.lr * (np.float32(1.0) / (np.float32(1.0) + self.decay * it)))
+        if self.precise:
+            lr_t = float(self.lr) / (1.0 + float(self.decay) * self.iterations)
+        else:
+            lr_t = float(self.lr * (np.float32(1.0) / (np.float32(1.0) + self.decay * it)))
         self.iterations += 1
         for k in params:
             g = grads[k]
             self.a[k] = float(self.rho) * self.a[k] + float(self.omr) * (g * g)
             params[k] = params[k] - lr_t * g / (torch.sqrt(self.a[k]) + float(self.eps))
+
+
+def fedavg_round(data, partner_rows, batch_sizes, coalition, glob, seed=0, M=20, e=0, m=0, precise=False):
+    """One FedAvg round of the CIFAR10 model from the global model `glob` (as oracle/cnn.py fedavg_round): each
+    partner a fresh Keras RMSprop over its round rows with the step's keyed dropout masks, then the data-volume
+    average.  precise=True: every tensor operation in float64 (same masks, schedule and constants)."""
+    torch = _torch()
+    coalition = tuple(sorted(coalition))
+    mask = sum(1 << p for p in coalition)
+    dt = torch.float64 if precise else torch.float32
+    sizes = [len(partner_rows[p]) for p in coalition]
+    w = np.asarray(sizes) / np.sum(sizes)
+    models = []
+    for p_id in coalition:
+        key = ocnn.shuffle_key(seed, mask, p_id)
+        params = {k: v.to(dt).clone() for k, v in glob.items()}
+        opt = KerasRMSprop(params, precise=precise)
+        for t, rows in enumerate(ocnn.fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m)):
+            masks = step_masks(fedavg_drop_key(key, e, m, t), len(rows))
+            g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks, dtype=dt if precise else None)
+            opt.step(params, g)
+        models.append(params)
+    return ocnn.average_models(glob, models, w, keep_f64=precise)
 
 
 def evaluate(p, x, y, batch=500):

@@ -218,12 +218,23 @@ def test_contributivity_tmcs_on_cifar():
 
 
 def test_empty_minibatch_partner_restarts_from_global_model():
-    """As tests/test_cnn_gpu.py for the CIFAR10 trainer's W5-broadcast skip."""
+    """a FedAvg partner with fewer rows than minibatch_count has empty minibatches; in those rounds
+    it trains nothing and enters the average with the round's global model (the reference builds it fresh
+    from the global weights, mplc/multi_partner_learning.py:319).  Scenario refuses such a split
+    (mplc/scenario.py's minibatch_count <= min(amounts) * n check), but the engine accepts any partner rows:
+    the dense-layer broadcast skip must not leave that partner a stale copy.  Values and final models equal
+    the plain copy-back path bit for bit."""
     from mplc.engine import CoalitionEngine
-    sc = make_scenario(partners=2, amounts=(0.01, 0.99), M=20, G=2, E=1)
-    assert len(sc.partners_list[0].train_idx) < 20
-    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
-    coals = [(0, 1), (1,)]
+    sc = make_scenario(partners=2, amounts=(0.3, 0.7), M=2, G=2, E=1)
+    d = sc.dataset
+    rows0 = list(sc.partners_list[0].train_idx[:13])  # 13 rows, 20 minibatches: 7 empty ones
+    rows1 = list(sc.partners_list[1].train_idx)
+    eng = CoalitionEngine(x_train=d.x_train, y_train=d.y_train, x_val=d.x_val, y_val=d.y_val, x_test=d.x_test,
+                          y_test=d.y_test, partner_rows=[rows0, rows1], batch_sizes=[1, 24], epoch_count=1,
+                          minibatch_count=20, is_early_stopping=False, model="cifar10_cnn",
+                          memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    assert any(b[m + 1] == b[m] for b in [eng.bounds[0]] for m in range(20))
+    coals = [(0, 1), (0,), (1,)]
     skip = eng.evaluate(coals, return_models=True, return_details=True)
     eng.bcast_skip = False
     full = eng.evaluate(coals, return_models=True, return_details=True)

@@ -357,14 +357,20 @@ def test_scenario_run_saves_final_model(tmp_path):
 def test_empty_minibatch_partner_restarts_from_global_model():
     """a FedAvg partner with fewer rows than minibatch_count has empty minibatches; in those rounds
     it trains nothing and enters the average with the round's global model (the reference builds it fresh
-    from the global weights, mplc/multi_partner_learning.py:319).  The W3-broadcast skip must not leave it a
-    stale W3: values equal the plain copy-back path bit for bit, with and without other coalitions in the
-    batch, and follow the oracle."""
+    from the global weights, mplc/multi_partner_learning.py:319).  Scenario refuses such a split
+    (mplc/scenario.py's minibatch_count <= min(amounts) * n check), but the engine accepts any partner rows:
+    the dense-layer broadcast skip must not leave that partner a stale copy.  Values and final models equal
+    the plain copy-back path bit for bit."""
     from mplc.engine import CoalitionEngine
-    sc = make_scenario(partners=2, amounts=(0.01, 0.99), M=20, G=2, E=1)
-    prow, bs = rows(sc)
-    assert len(prow[0]) < 20  # empty splits for partner 0
-    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    sc = make_scenario(partners=2, amounts=(0.3, 0.7), M=2, G=2, E=1)
+    d = sc.dataset
+    rows0 = list(sc.partners_list[0].train_idx[:13])  # 13 rows, 20 minibatches: 7 empty ones
+    rows1 = list(sc.partners_list[1].train_idx)
+    eng = CoalitionEngine(x_train=d.x_train, y_train=d.y_train, x_val=d.x_val, y_val=d.y_val, x_test=d.x_test,
+                          y_test=d.y_test, partner_rows=[rows0, rows1], batch_sizes=[1, 24], epoch_count=1,
+                          minibatch_count=20, is_early_stopping=False, model="mnist_cnn",
+                          memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
+    assert any(b[m + 1] == b[m] for b in [eng.bounds[0]] for m in range(20))
     coals = [(0, 1), (0,), (1,)]
     skip = eng.evaluate(coals, return_models=True, return_details=True)
     eng.bcast_skip = False
@@ -372,9 +378,8 @@ def test_empty_minibatch_partner_restarts_from_global_model():
     assert np.array_equal(skip["scores"], full["scores"])
     for a, b in zip(skip["models"][0], full["models"][0]):
         assert np.array_equal(a, b)
-    ds = sc.dataset
-    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    ref, _ = ocnn.coalition_value(data, prow, bs, (0, 1), seed=eng.seed, epochs=1, M=20)
+    data = ocnn.Data(d.x_train, d.y_train, d.x_val, d.y_val, d.x_test, d.y_test)
+    ref, _ = ocnn.coalition_value(data, [rows0, rows1], [1, 24], (0, 1), seed=eng.seed, epochs=1, M=20)
     assert abs(skip["scores"][0] - ref) <= 0.03, (skip["scores"][0], ref)
 
 

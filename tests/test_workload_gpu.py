@@ -226,7 +226,14 @@ def test_config4_smc_batched_equals_sequential_reference_loop(cifar10p, config4_
 
 def test_config4_smc_values_are_engine_values_and_vs_oracle(cifar10p, config4_smc):
     """Every memo entry is the engine's v(S) for that coalition (re-evaluated alone: bit-identical), and two
-    coalitions the SMCS run drew follow oracle/cifar_cnn.py (sequential, same keys and schedule)."""
+    coalitions the SMCS run drew (the memo's first and last |S| <= 2 entries) follow oracle/cifar_cnn.py
+    (sequential, same keys, schedule and dropout masks).  At E=1 these CIFAR models sit in the steep start of
+    learning (accuracy ~0.3), where the fp32 summation order alone moves a coalition by points: the oracle
+    itself gives 0.2202 (8 CPU threads) vs 0.2765 (3 threads) for (6, 8) in the build container, and 0.3071
+    with the GPU box's 16 (one round's fp32-vs-fp64 error of the oracle moves between 4e-4 and 5e-2 with the
+    thread count: max-pool near-ties route a gradient differently and RMSprop's normalisation spreads it).  So
+    the device must land inside the oracle's own spread over thread counts (3, 8 and the box's), widened by
+    1 pt."""
     from oracle import cifar_cnn as occ
     c = config4_smc["SMCS"]
     eng = cifar10p.engine
@@ -239,9 +246,16 @@ def test_config4_smc_values_are_engine_values_and_vs_oracle(cifar10p, config4_sm
     data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow = [p.train_idx for p in cifar10p.partners_list]
     bs = [p.batch_size for p in cifar10p.partners_list]
-    ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in picks])
-    diff = np.abs(np.asarray(dev) - ref)
-    assert np.max(diff) <= 0.03, (picks, dev, ref)
+    import torch
+    threads0 = torch.get_num_threads()
+    refs = []
+    for th in sorted({3, 8, threads0}):
+        torch.set_num_threads(th)
+        refs.append([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in picks])
+    torch.set_num_threads(threads0)
+    refs = np.array(refs)
+    lo, hi = refs.min(axis=0) - 0.01, refs.max(axis=0) + 0.01
+    assert np.all((lo <= dev) & (dev <= hi)), (picks, dev, refs)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -252,8 +266,12 @@ def test_config3_round_trajectory_vs_fp64(mnist10):
     minibatch, then the data-volume average) on the Winograd kernels, against the oracle's schedule run in
     fp64 (oracle/cnn.py fedavg_round(precise=True)) from the same keyed initial model.  Per tensor, the
     device's error on the round's update, ||dev - ref64|| / ||ref64 - start||, must be <= 4x the oracle's own
-    fp32 run's error on the same round: this pins the kernels' rounding (Winograd transforms, MFMA
-    accumulation order, the fused Adam) with no accuracy noise in the way."""
+    fp32 error on the same round: this pins the kernels' rounding (Winograd transforms, MFMA accumulation
+    order, the fused Adam) with no accuracy noise in the way.  The fp32 oracle's error is itself
+    a spread over summation orders: run with 1, 2, 3 and 8 CPU threads (build container) W1's error moves
+    1.3e-6 .. 4.2e-6 and W4's 6.5e-6 .. 1.1e-5 (W4's 1290-element update is dominated by a few weights whose
+    gradient sits near Adam's eps, where lr * g / (|g| + eps) amplifies rounding), so the reference value per
+    tensor is the largest error of the oracle run at 1, 2, 3 and the box's thread count."""
     import torch
     from oracle import cnn as ocnn
     from mplc.engine import CoalitionEngine
@@ -273,15 +291,20 @@ def test_config3_round_trajectory_vs_fp64(mnist10):
     bs = [p.batch_size for p in mnist10.partners_list]
     glob = ocnn.unpack(start)
     assert np.array_equal(start, ocnn.init_params(ocnn.init_key(eng.seed, sum(1 << p for p in coal))))
-    g32 = ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=20)
     g64 = ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=20, precise=True)
+    threads0 = torch.get_num_threads()
+    g32s = []
+    for th in sorted({1, 2, 3, threads0}):
+        torch.set_num_threads(th)
+        g32s.append(ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=20))
+    torch.set_num_threads(threads0)
     report, bad = [], []
     for name, (off, shape) in ocnn.OFF.items():
         n = int(np.prod(shape))
         ref = g64[name].numpy().reshape(-1)
         upd = np.linalg.norm(ref - start[off:off + n].astype(np.float64))
         err_dev = np.linalg.norm(dev[off:off + n].astype(np.float64) - ref) / upd
-        err_cpu = np.linalg.norm(g32[name].numpy().reshape(-1).astype(np.float64) - ref) / upd
+        err_cpu = max(np.linalg.norm(g[name].numpy().reshape(-1).astype(np.float64) - ref) / upd for g in g32s)
         report.append((name, float(err_dev), float(err_cpu)))
         if not err_dev <= 4 * err_cpu:
             bad.append(report[-1])
