@@ -361,14 +361,14 @@ def cpu_baseline_shapley(n_sample=24):
 # --------------------------------------------------------------------------------------------------
 # training leg (config #3)
 # --------------------------------------------------------------------------------------------------
-def build_scenario(partners, epochs, M, G):
+def build_scenario(partners, epochs, M, G, early_stopping=False, signal=0.0):
     from mplc.dataset import Mnist
     from mplc.scenario import Scenario
     amounts = [1.0 / partners] * partners
     if partners == 10:
         amounts = [0.1] * 10
-    sc = Scenario(partners, amounts, dataset=Mnist(synthetic=True), minibatch_count=M,
-                  gradient_updates_per_pass_count=G, epoch_count=epochs, is_early_stopping=False)
+    sc = Scenario(partners, amounts, dataset=Mnist(synthetic=True, signal=signal), minibatch_count=M,
+                  gradient_updates_per_pass_count=G, epoch_count=epochs, is_early_stopping=early_stopping)
     return sc.provision()
 
 
@@ -476,11 +476,17 @@ def bench_train(args, rank, world):
     import numpy as np
     from mplc.contributivity import Contributivity
     from mplc.profiling import KernelTimer
-    sc = build_scenario(args.partners, args.epochs, args.minibatches, args.gupp)
+    sc = build_scenario(args.partners, args.epochs, args.minibatches, args.gupp, args.early_stopping,
+                        args.mnist_signal)
     from mplc.engine import CoalitionEngine
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
     eng.warmup()  # untimed: code-object load (no training launch, so rocprof averages = timed launches)
+
+    def progress(s, total, R):  # heartbeat for long sweeps (E=40: one sweep is several minutes)
+        if s % 600 == 0 and total > 1000:
+            log(f"train: lockstep step {s}/{total} ({R} replicas)")
+    eng.progress = progress
     n = args.partners
     n_coal = 2 ** n - 1
     log(f"train leg ready: {n} partners, {n_coal} coalitions")
@@ -571,6 +577,24 @@ def bench_train(args, rank, world):
         "first_charac_fct_calls_count": int(c.first_charac_fct_calls_count),
         "epochs_per_coalition": args.epochs,
     }
+    if args.early_stopping:
+        # the reference's defaults (E=40, early stopping, mplc/constants.py:10-12): realised epochs per coalition,
+        # the per-epoch val evaluations the stopping rule needs, and the lockstep batch's idle replica-steps
+        # (stopped coalitions wait for the batch's last one)
+        ep = np.array(eng.last_epochs_done, dtype=np.float64)
+        st_ = eng.stats
+        out["early_stopping"] = {
+            "epochs_max": args.epochs, "realised_epochs_mean": round(float(ep.mean()), 2),
+            "realised_epochs_min": int(ep.min()), "realised_epochs_max": int(ep.max()),
+            "realised_epochs_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(ep, return_counts=True))},
+            "val_eval_s_per_step": round(st_.get("es_val_s", 0.0) / max(1, steps + warm), 2),
+            "val_eval_share": round(st_.get("es_val_s", 0.0) / max(1e-9, (steps + warm) * ms_per_step / 1000), 4),
+            "replica_steps_idle_share": round(1 - st_.get("replica_steps_live", 0) / max(1, st_.get("replica_steps", 1)),
+                                              4),
+            "data": f"learnable synthetic MNIST (class templates, signal {args.mnist_signal})"}
+        out["epochs_per_coalition"] = None
+        out["config"]["workload"] = out["config"]["workload"].replace(f"E={args.epochs} fixed",
+                                                                      f"E<={args.epochs} + early stopping")
     # whole-job algorithmic rate: training 2*E*sum n_p samples x 71.57 MFLOP + test evaluation
     # 1023 x 10000 x 23.98 MFLOP (MNIST CNN forward / train FLOPs per sample)
     job_flop = total_train_samples / steps * MNIST_TRAIN_FLOP + n_coal * len(sc.dataset.x_test) * MNIST_FWD_FLOP
@@ -592,6 +616,34 @@ def build_cifar_scenario(epochs, signal, partners=20):
     sc = Scenario(partners, amounts, dataset=Cifar10(synthetic=True, signal=signal), minibatch_count=20,
                   gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False)
     return sc.provision()
+
+
+def cifar_kernel_table(timer, units):
+    """Config #4's per-kernel table (as kernel_table for config #3): launches, in-stream ms, time share, and for
+    the convolutions (their algorithm's FLOPs: Winograd for conv2..conv4) and the W5 kernels (HBM bytes,
+    CifarModel.algorithmic_units) the achieved rate against the roofline."""
+    from mplc.cifar import FLOP_PER_SAMPLE, KERNEL_IDS
+    tot = sum(timer.total_ms(k) for k in KERNEL_IDS) or 1.0
+    out = {}
+    for k in KERNEL_IDS:
+        ms, n = timer.total_ms(k), timer.launches(k)
+        e = {"launches": n, "ms_total": round(ms, 1), "ms_avg": round(ms / max(1, n), 4), "time_share": round(ms / tot, 4)}
+        if ms > 0 and units:
+            if k in FLOP_PER_SAMPLE:
+                amount = units["samples"] * FLOP_PER_SAMPLE[k]
+                rate, peak, unit, bound = amount / (ms / 1000) / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+                desc = f"{k}'s fp32 multiply-adds ({FLOP_PER_SAMPLE[k]} per sample)"
+            elif f"{k}_bytes" in units:
+                amount = units[f"{k}_bytes"]
+                rate, peak, unit, bound = amount / (ms / 1000) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+                desc = f"{k}'s algorithmic HBM bytes (W5 + RMSprop state by optimizer step, per-sample rows)"
+            else:
+                out[k] = e
+                continue
+            e.update({"bound": bound, "achieved": round(rate, 2), "peak": peak, "unit": unit,
+                      "frac": round(rate / peak, 4), "units_per_launch": int(amount / max(1, n)), "algorithmic": desc})
+        out[k] = e
+    return out
 
 
 def cpu_baseline_cifar(sc, coalitions, epochs, M):
@@ -626,7 +678,7 @@ def bench_cifar(args, rank, world, sub=False):
     TMCS run, no warm-up step (the code object is loaded by eng.warmup(); each lockstep batch allocates its
     own buffers anyway)."""
     import numpy as np
-    from mplc.cifar import FLOP_PER_SAMPLE
+    from mplc.cifar import DIRECT_FLOP_PER_SAMPLE, FLOP_PER_SAMPLE
     from mplc.contributivity import Contributivity
     from mplc.engine import CoalitionEngine
     from mplc.profiling import KernelTimer
@@ -639,7 +691,8 @@ def bench_cifar(args, rank, world, sub=False):
         if s == 0:
             log(f"cifar: batch of {R} replicas, {total} steps, {eng.stats['coalitions']} coalitions so far")
     eng.progress = progress
-    timer = KernelTimer(args.cifar_profile_kernel)
+    from mplc.cifar import KERNEL_IDS as CIFAR_KERNEL_IDS
+    timer = KernelTimer("all", list(CIFAR_KERNEL_IDS), stash=True)
     s0 = [0]
 
     def one_step():
@@ -650,9 +703,9 @@ def bench_cifar(args, rank, world, sub=False):
         return c
 
     def timed_step(i, planned):
-        if eng.profiler is None:
-            eng.profiler = timer
-            s0[0] = eng.stats["samples"]
+        if s0[0] == 0:
+            eng.profiler = None if args.no_kernel_timer else timer
+            s0[0] = eng.stats["samples"] or -1
         return one_step()
 
     if sub:
@@ -661,9 +714,12 @@ def bench_cifar(args, rank, world, sub=False):
         reserve = (60 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
         steps, warm, wall, c, _ = run_budgeted(one_step, timed_step, args, world, reserve, "cifar")
     eng.profiler = None
-    kern_ms = timer.total_ms()
-    launches = timer.launches()
-    samples = eng.stats["samples"] - s0[0]
+    units = eng.model_impl.algorithmic_units(timer.stash)
+    timer.stash = []
+    kernels = cifar_kernel_table(timer, units) if not args.no_kernel_timer else {}
+    kern_ms = timer.total_ms(args.cifar_profile_kernel)
+    launches = timer.launches(args.cifar_profile_kernel)
+    samples = eng.stats["samples"] - max(0, s0[0])
     flops = samples * FLOP_PER_SAMPLE[args.cifar_profile_kernel]
     achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
     evals = c.first_charac_fct_calls_count
@@ -690,8 +746,25 @@ def bench_cifar(args, rank, world, sub=False):
                      "kernel": args.cifar_profile_kernel, "launches": launches,
                      "kernel_ms_avg": round(kern_ms / max(1, launches), 4),
                      "algorithmic_flop_per_launch": int(flops / max(1, launches)),
-                     "flop_per_sample": FLOP_PER_SAMPLE[args.cifar_profile_kernel]},
+                     "flop_per_sample": FLOP_PER_SAMPLE[args.cifar_profile_kernel],
+                     "direct_equivalent_tflops": round(achieved * DIRECT_FLOP_PER_SAMPLE[args.cifar_profile_kernel]
+                                                       / FLOP_PER_SAMPLE[args.cifar_profile_kernel], 2),
+                     "note": "achieved = the kernel's own (Winograd F(2x2,3x3)) fp32 multiply-adds / in-stream "
+                             "kernel time; direct_equivalent_tflops prices the same time at the direct "
+                             "convolution's count"},
+        "kernels": kernels,
     }
+    # the roofline on the step's dominant kernel (largest share of the kernel time), as the config #3 line
+    dom = max((k for k in kernels if "frac" in kernels[k]), key=lambda k: kernels[k]["ms_total"], default=None)
+    if dom is not None:
+        kd = kernels[dom]
+        out["roofline_conv2_fwd"] = out["roofline"]
+        out["roofline"] = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
+                           "frac": kd["frac"], "traffic": None, "kernel": dom, "launches": kd["launches"],
+                           "kernel_ms_avg": kd["ms_avg"], "time_share": kd["time_share"],
+                           "units_per_launch": kd["units_per_launch"],
+                           "note": "the step's dominant kernel; achieved = " + kd["algorithmic"] +
+                                   " / in-stream kernel time (HIP events on the launch stream)"}
     return out, sc, coals
 
 
@@ -716,9 +789,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shapley-agg", action="store_true")
     ap.add_argument("--no-cifar", action="store_true", help="leave out the config #4 sub-leg of the default line")
+    ap.add_argument("--early-stopping", action="store_true",
+                    help="train leg at the reference's stopping rule (with --epochs 40: its defaults)")
+    ap.add_argument("--mnist-signal", type=float, default=0.0,
+                    help="class-template signal of the synthetic MNIST (0: random labels)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()
+    if os.environ.get("ROCPROF_COUNTER_COLLECTION", "").lower() in ("1", "true", "yes") and \
+            not os.environ.get("MPLC_FORCE_KERNEL_TIMER"):
+        # under `rocprofv3 --pmc` the in-stream HIP events are left out: round 2 saw rocprofv3's counter thread
+        # crash (SIGSEGV) on a --pmc pass of this bench with an event record around every launch
+        # (profiles/r03_pmc_events_crash.txt); the counter passes need the kernels, not the timer
+        args.no_kernel_timer = True
+        log("rocprofv3 counter collection detected: in-stream kernel timer off")
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -464,6 +464,289 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// 3x3 stride-1 convolution in Winograd form F(2x2, 3x3) (Lavin & Gray) on v_mfma_f32_16x16x4_f32, for the
+// layers with CI >= 32 (conv2..conv4 forward, and their data gradients = forward convolutions of dZ with the
+// rotated, channel-swapped kernel, padding 2 - PAD):
+//   out tile (2x2) = A^T [ (G g G^T) (.) (B^T d B) ] A  per 4x4 input patch d, summed over the input channels
+// as 16 GEMMs M[xi][tile][co] = sum_ci V[xi][tile][ci] U[xi][ci][co]: 2.25x fewer multiply-adds than the
+// direct implicit GEMM (16 per output tile of 4 instead of 36).  Everything stays fp32 (the transforms'
+// coefficients are 0, +-1, +-1/2, exact; accumulation on the exact-f32 MFMA).  U is the per-replica,
+// per-step Winograd form of the layer's weights (wino_u_kernel), read from L2.
+// Tiles: the output in 2x2 tiles; for the pooled forward one tile IS one 2x2 max-pool window (pool = max
+// over the tile's 4 outputs, no row/column of the unpooled output is computed that the pool drops).
+// Block = (band of BTY tile rows, sample slot j, replica r), 4 waves; the band's input rows (zero padded)
+// are staged in LDS once ([rows][cols][CI + 1]: the 32 lanes of a half-wave read 16 tiles x 2 channels on
+// 32 banks).  Wave i owns transform row i (xi = 4i .. 4i+3) of every 16-tile group and all CO channels:
+// 4 x CO/16 accumulators of 16x16x4; per k-step (4 input channels) a lane reads 8 staged values of its
+// tile's patch, forms its 4 values of V with 12 adds and issues 4 x CO/16 MFMAs, the B operands (U) loaded
+// one k-step ahead.  The waves fold their row of the output transform (T_i = M_i A) into LDS (32 output
+// channels at a time); then every thread finishes Y = A^T T for (tile, channel) items and applies the layer's
+// epilogue (same semantics as conv_kernel's).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) {  // o = G g (one column)
+  o[0] = g[0];
+  o[1] = 0.5f * ((g[0] + g[1]) + g[2]);
+  o[2] = 0.5f * ((g[0] - g[1]) + g[2]);
+  o[3] = g[2];
+}
+
+// U[xi][cin][cout] = (G g G^T)[i][j], xi = 4i + j, for the kernel g of channel pair (cin, cout):
+// FLIP = 0: the layer's forward kernel, g[ky][kx] = W[ky][kx][cin][cout];
+// FLIP = 1: the data gradient's kernel, g[ky][kx] = W[2 - ky][2 - kx][cout][cin] (in = the layer's co).
+template <int CIN, int COUT, int FLIP>
+__device__ __forceinline__ void wino_u_pair(const float* __restrict__ W, float* __restrict__ U, int e) {
+  const int cin = e / COUT, cout = e % COUT;
+  float g[3][3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+      g[ky][kx] = FLIP ? W[((2 - ky) * 3 + (2 - kx)) * CIN * COUT + cout * CIN + cin]
+                       : W[(ky * 3 + kx) * CIN * COUT + cin * COUT + cout];
+  float gg[4][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const float col[3] = {g[0][kx], g[1][kx], g[2][kx]};
+    float o[4];
+    wino_g_rows(col, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float o[4];
+    wino_g_rows(gg[i], o);
+#pragma unroll
+    for (int jx = 0; jx < 4; ++jx) U[(4 * i + jx) * CIN * COUT + e] = o[jx];
+  }
+}
+
+// Winograd-form weights of conv2 | conv3 | conv4 (layout MPLC_CIFAR_WT: WU_2, WU_3, WU_4) for the forward
+// (FLIP = 0) or the data gradients (FLIP = 1), one thread per channel pair.
+constexpr int WU_2 = 0, WU_3 = 16 * 32 * 32, WU_4 = WU_3 + 16 * 32 * 64;
+static_assert(WU_4 + 16 * 64 * 64 == MPLC_CIFAR_WT, "MPLC_CIFAR_WT must hold conv2..conv4 in Winograd form");
+
+template <int FLIP>
+__global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ params, int64_t stride,
+                                                     const int32_t* __restrict__ cnt, float* __restrict__ U) {
+  const int r = blockIdx.y;
+  if (cnt && cnt[r] == 0) return;
+  const int e = blockIdx.x * 256 + threadIdx.x;  // pair index over conv2 (1024) | conv3 (2048) | conv4 (4096)
+  const float* P = params + (int64_t)r * stride;
+  float* Ur = U + (int64_t)r * MPLC_CIFAR_WT;
+  if (e < 1024) {
+    wino_u_pair<32, 32, FLIP>(P + OFF_W2, Ur + WU_2, e);
+  } else if (e < 3072) {
+    if (FLIP) wino_u_pair<64, 32, 1>(P + OFF_W3, Ur + WU_3, e - 1024);   // dgrad: in = conv3's 64 co
+    else wino_u_pair<32, 64, 0>(P + OFF_W3, Ur + WU_3, e - 1024);
+  } else if (e < 7168) {
+    wino_u_pair<64, 64, FLIP>(P + OFF_W4, Ur + WU_4, e - 3072);
+  }
+}
+
+template <int HI, int WI, int CI, int CO, int PAD, int BTY, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_kernel(const ConvArgs a) {
+  constexpr bool POOL = (EPI == EPI_FWD_POOL);
+  constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
+  constexpr int PH = HO / 2, PW = WO / 2;
+  constexpr int TYT = POOL ? PH : (HO + 1) / 2;  // tile rows / columns computed
+  constexpr int TXT = POOL ? PW : (WO + 1) / 2;
+  constexpr int NG = (BTY * TXT + 15) / 16;      // 16-tile groups per band
+  constexpr int LR = 2 * BTY + 2, LC = 2 * TXT + 2;
+  constexpr int CIP = CI + 1;                    // odd channel stride
+  constexpr int ROWP = LC * CIP;
+  constexpr int NCG = CO / 16;
+  constexpr int CH = CO > 32 ? 32 : CO;          // output channels per output-transform pass
+  constexpr int NPASS = CO / CH;
+  constexpr int TS = CH + 1;
+  constexpr int TQ = 16 * TS;
+  constexpr int NK = CI / 4;
+  static_assert(CI % 4 == 0 && CO % 32 == 0, "channel counts");
+  static_assert((16 * CH) % 256 == 0, "output items per thread");
+  __shared__ float in_s[LR * ROWP];
+  __shared__ float t_s[8 * TQ];
+  const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+  const int count = a.cnt ? a.cnt[r] : a.cnt_all;
+  if (j >= count) return;
+  const int tid = threadIdx.x;
+  const int64_t slot = (int64_t)r * a.bmax + j;
+  constexpr int IN_SZ = HI * WI * CI;
+  const float* src = a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ : a.in + slot * IN_SZ;
+  const int ty0 = band * BTY;
+  const int bty = min(BTY, TYT - ty0);  // tile rows of this band
+  const int ntile = bty * TXT;
+  {  // stage input rows 2 ty0 - PAD .. + LR, columns -PAD .. + LC (zero outside the input)
+    constexpr int C4 = CI / 4;
+    constexpr int TOT = LR * LC * C4;
+    constexpr int NIT = (TOT + 255) / 256;
+    fvec4 v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e4 = tid + k * 256;
+      const int pix = e4 / C4, c4 = e4 % C4;
+      const int iy = 2 * ty0 - PAD + pix / LC, ix = pix % LC - PAD;
+      const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+      const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? src + (iy * WI + ix) * CI + 4 * c4 : src);
+      v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e4 = tid + k * 256;
+      if (e4 < TOT) {
+        const int pix = e4 / C4, c4 = e4 % C4;
+        float* d = in_s + pix * CIP + 4 * c4;
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
+      }
+    }
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wi = wave;
+  const int tl = lane & 15, kq = lane >> 4;
+  // B^T row i combines patch rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  const int drow = (rb - ra) * ROWP;
+  const float* Ub = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + kq * CO + tl;
+  auto load_b = [&](int st, float (&bv)[4 * NCG]) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) bv[NCG * jj + cg] = Ub[(int64_t)jj * CI * CO + (4 * st) * CO + 16 * cg];
+  };
+  float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
+  const float* bias = (EPI == EPI_FWD || POOL) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
+  const float* act = (EPI == EPI_BWD_MASK) ? a.aux + slot * (HO * WO * CO) : nullptr;
+  const uint8_t* cd = (EPI == EPI_BWD_UNPOOL) ? a.code_in + slot * (HO * WO * CO) : nullptr;
+  uint8_t* oc = (POOL && a.drop_key) ? a.code_out + slot * (PH * PW * CO) : nullptr;
+  const uint32_t rseed = (POOL && a.drop_key) ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
+  __syncthreads();
+#pragma unroll 1
+  for (int g = 0; g < NG; ++g) {
+    if (16 * g >= ntile) break;  // block-uniform
+    const int tile = min(16 * g + tl, ntile - 1);
+    const int tyl = tile / TXT, tx = tile % TXT;
+    const float* dpa = in_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP + kq;
+    fvec4 acc[4][NCG];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) acc[jj][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    // k-steps in pairs with two B buffers (the next step's operands in flight during this step's MFMAs);
+    // not unrolled further: a fully unrolled CI = 64 loop lets the scheduler hoist every load and spill
+    auto kstep = [&](int st, const float (&bv)[4 * NCG]) {
+      const float* d0 = dpa + 4 * st;
+      float t[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * CIP] + sb * d0[drow + c * CIP];
+      float v[4];
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) acc[jj][cg] = mfma16(v[jj], bv[NCG * jj + cg], acc[jj][cg]);
+    };
+    static_assert(NK % 2 == 0, "k-steps in pairs");
+    float b0[4 * NCG], b1[4 * NCG];
+    load_b(0, b0);
+#pragma unroll 1
+    for (int st = 0; st < NK; st += 2) {
+      load_b(st + 1, b1);
+      kstep(st, b0);
+      if (st + 2 < NK) load_b(st + 2, b0);
+      kstep(st + 1, b1);
+    }
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+      // T_i[b] = sum_j M_ij A[j][b]: lane holds tiles 4 kq + rr of the group, channel 16 cg + tl
+#pragma unroll
+      for (int cgl = 0; cgl < CH / 16; ++cgl)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int cg = pass * (CH / 16) + cgl;
+          const float m0 = acc[0][cg][rr], m1 = acc[1][cg][rr], m2 = acc[2][cg][rr], m3 = acc[3][cg][rr];
+          const int off = (4 * kq + rr) * TS + 16 * cgl + tl;
+          t_s[(2 * wi) * TQ + off] = (m0 + m1) + m2;
+          t_s[(2 * wi + 1) * TQ + off] = (m1 - m2) - m3;
+        }
+      __syncthreads();
+      // Y[a][b] = sum_i A^T[a][i] T_i[b]: Y0b = T0b + T1b + T2b, Y1b = T1b - T2b - T3b; tile pixel q = 2a + b
+#pragma unroll
+      for (int k = 0; k < 16 * CH / 256; ++k) {
+        const int it = tid + 256 * k;
+        const int col = it % CH, tg = it / CH;
+        const int tt = 16 * g + tg;
+        const int co = pass * CH + col;
+        float tv[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * TQ + tg * TS + col];
+        float y[4];
+        y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
+        y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
+        y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
+        y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
+        if (tt < ntile) {
+          const int ty = ty0 + tt / TXT, tx2 = tt % TXT;
+          if constexpr (POOL) {
+            const float bv = bias[co];
+            float best = y[0] + bv;
+            int arg = 0;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const float z = y[q] + bv;
+              if (z > best) { best = z; arg = q; }
+            }
+            const int pidx = (ty * PW + tx2) * CO + co;
+            const float av = fmaxf(best, 0.0f);
+            if (oc) {
+              const bool keep = drop_keep(rseed, (uint32_t)pidx, THR_25);
+              o[pidx] = keep ? av * SCALE_25 : 0.0f;
+              oc[pidx] = (uint8_t)(arg | (keep ? CODE_KEEP : 0) | (best > 0.0f ? CODE_POS : 0));
+            } else {
+              o[pidx] = av;
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int yy = 2 * ty + (q >> 1), xx = 2 * tx2 + (q & 1);
+              if (yy >= HO || xx >= WO) continue;
+              const int o_i = (yy * WO + xx) * CO + co;
+              if constexpr (EPI == EPI_FWD) {
+                o[o_i] = fmaxf(y[q] + bias[co], 0.0f);
+              } else if constexpr (EPI == EPI_BWD_MASK) {
+                o[o_i] = act[o_i] > 0.0f ? y[q] : 0.0f;
+              } else {  // dropout' + un-pool into the dense dZ (2HO x 2WO) of the layer below
+                const uint32_t c = cd[o_i];
+                const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
+                const bool pos = (c & CODE_POS) != 0;
+                const int sel = c & 3;
+#pragma unroll
+                for (int p4 = 0; p4 < 4; ++p4)
+                  o[((2 * yy + (p4 >> 1)) * (2 * WO) + 2 * xx + (p4 & 1)) * CO + co] = (pos && sel == p4) ? dv : 0.0f;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Weight gradient of a 3x3 conv: dW[kyx][ci][co] = sum_{samples, pixels} X[p + (ky,kx) - PAD][ci] dZ[p][co],
 // db[co] = sum dZ.  Block = (split sp, replica r): samples [WGS*sp, WGS*sp + WGS) in order, row bands of BR
 // output rows; X band and dZ band staged in LDS (dZ rows padded to an even width WOE with zeros so a
@@ -655,6 +938,207 @@ void wgrad_kernel(const WgArgs a) {
     constexpr int Z4 = CO / 4;
     float s = 0.0f;
     for (int i = 0; i < NTHR / Z4; ++i) s += gb_s[tid / 4 + Z4 * i][tid % 4];
+    out[a.off_b + tid] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient of conv2..conv4 in Winograd form F(3x3, 2x2) (the transposed dual of the forward's
+// F(2x2, 3x3)): with Y = A^T [U (.) V] A per 2x2 output tile, dL/dU = (A dY A^T) (.) V, so
+//   dW[3x3] = G^T [ sum_tiles (A dY A^T) (.) (B^T d B) ] G
+// per (ci, co), the sum over the tiles of the split's samples running in the transformed domain as 16 GEMMs
+// M[xi][ci][co] = sum_tiles V[xi][tile][ci] D[xi][tile][co] on v_mfma_f32_16x16x4_f32 (K = tiles, 4 per
+// k-step): 2.25x fewer multiply-adds than the direct sum.  Only the first HOV x WOV output pixels enter
+// (conv4: row / column 12 are dropped by the pool, their dZ is 0); the tile grid covers them (zero beyond).
+// Block = (split sp, replica r, input-channel chunk of CIB), 4 waves; wave i owns transform row i (xi = 4i ..
+// 4i+3): 4 x CIB/16 x CO/16 accumulators.  Per band (BTY tile rows of one sample) the input rows (channels of
+// the chunk) and the dZ rows are staged in LDS; per k-step a lane forms V of its tile for CIB/16 channels
+// (8 reads, 12 adds each) and D = A dY A^T for CO/16 channels (4 reads, 6 adds each).  At the end the waves
+// fold their row of the inverse transform (P_i = M_i G) and exchange it through LDS, 16 input channels at a
+// time.  Samples, bands and tiles in a fixed order: sums independent of which replicas share the launch.
+// ------------------------------------------------------------------------------------------------
+template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BTY, int CIB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wgrad_kernel(const WgArgs a) {
+  constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
+  constexpr int TY = (HOV + 1) / 2, TX = (WOV + 1) / 2;
+  constexpr int NB = (TY + BTY - 1) / BTY;
+  constexpr int LR = 2 * BTY + 2, LC = 2 * TX + 2;
+  constexpr int CIP = CIB + 1;
+  constexpr int XROW = LC * CIP;
+  constexpr int ZR = 2 * BTY, ZC = 2 * TX;
+  constexpr int COP = CO + 1;
+  constexpr int NH = CIB / 16, NCG = CO / 16;
+  constexpr int XS = LR * XROW, ZS = ZR * ZC * COP;
+  constexpr int PS = 4 * 3 * 16 * CO;  // the four waves' P_i for 16 input channels
+  constexpr int SM = (XS + ZS > PS) ? XS + ZS : PS;
+  static_assert(CI % CIB == 0 && CIB % 16 == 0 && CO % 16 == 0, "channel chunks");
+  __shared__ float smem[SM];
+  __shared__ fvec4 gb_s[256];
+  float* const x_s = smem;
+  float* const z_s = smem + XS;
+  const int sp = blockIdx.x, r = blockIdx.y, chn = blockIdx.z;
+  const int count = a.cnt[r];
+  const int j_begin = sp * WGS, j_end = min(count, j_begin + WGS);
+  if (j_begin >= j_end) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wi = wave;
+  const int tl = lane & 15, kq = lane >> 4;
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  const float ai0 = (wi == 3) ? 0.0f : 1.0f;                       // A[i][0]
+  const float ai1 = (wi == 0) ? 0.0f : ((wi == 1) ? 1.0f : -1.0f);  // A[i][1]
+  const int drow = (rb - ra) * XROW;
+  fvec4 acc[4][NH][NCG];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  fvec4 gb = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // db partial of channels 4 * (tid % (CO / 4)) .. + 3
+  for (int j = j_begin; j < j_end; ++j) {
+    const int64_t slot = (int64_t)r * a.bmax + j;
+    const float* X = a.x + slot * (HI * WI * CI) + chn * CIB;
+    const float* Z = a.dz + slot * (HO * WO * CO);
+#pragma unroll 1
+    for (int band = 0; band < NB; ++band) {
+      const int ty0 = band * BTY;
+      const int bty = min(BTY, TY - ty0);
+      __syncthreads();  // the previous band's readers are done
+      {  // input rows 2 ty0 - PAD .., columns -PAD .., this chunk's channels (zero outside the input)
+        constexpr int C4 = CIB / 4;
+        constexpr int TOT = LR * LC * C4;
+        constexpr int NIT = (TOT + 255) / 256;
+        fvec4 v[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * 256;
+          const int pix = e4 / C4, c4 = e4 % C4;
+          const int iy = 2 * ty0 - PAD + pix / LC, ix = pix % LC - PAD;
+          const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? X + (iy * WI + ix) * CI + 4 * c4 : X);
+          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * 256;
+          if (e4 < TOT) {
+            float* d = x_s + (e4 / C4) * CIP + 4 * (e4 % C4);
+            d[0] = v[k].x;
+            d[1] = v[k].y;
+            d[2] = v[k].z;
+            d[3] = v[k].w;
+          }
+        }
+      }
+      {  // dZ rows 2 ty0 .. (zero beyond HOV x WOV); db from the same loads (chunk 0 only)
+        constexpr int Z4 = CO / 4;
+        constexpr int TOT = ZR * ZC * Z4;
+        constexpr int NIT = (TOT + 255) / 256;
+        static_assert(256 % Z4 == 0, "db needs a fixed channel quad per thread");
+        fvec4 v[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * 256;
+          const int pix = e4 / Z4, c4 = e4 % Z4;
+          const int yy = 2 * ty0 + pix / ZC, xx = pix % ZC;
+          const bool ok = e4 < TOT && yy < HOV && xx < WOV;
+          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? Z + (yy * WO + xx) * CO + 4 * c4 : Z);
+          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int e4 = tid + k * 256;
+          if (e4 < TOT) {
+            float* d = z_s + (e4 / Z4) * COP + 4 * (e4 % Z4);
+            d[0] = v[k].x;
+            d[1] = v[k].y;
+            d[2] = v[k].z;
+            d[3] = v[k].w;
+            gb += v[k];  // rows beyond HOV / WOV load 0
+          }
+        }
+      }
+      __syncthreads();
+      const int ntile = bty * TX;
+#pragma unroll 1
+      for (int t0 = 0; t0 < ntile; t0 += 4) {
+        const int tile = t0 + kq;
+        const bool ok = tile < ntile;
+        const int tc = ok ? tile : 0;
+        const int tyl = tc / TX, tx = tc % TX;
+        float va[NH][4];
+        const float* d0 = x_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP + tl;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          float t[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * CIP + 16 * h] + sb * d0[drow + c * CIP + 16 * h];
+          va[h][0] = ok ? t[0] - t[2] : 0.0f;
+          va[h][1] = ok ? t[1] + t[2] : 0.0f;
+          va[h][2] = ok ? t[2] - t[1] : 0.0f;
+          va[h][3] = ok ? t[1] - t[3] : 0.0f;
+        }
+        float db[NCG][4];
+        const float* z0 = z_s + ((2 * tyl) * ZC + 2 * tx) * COP + tl;
+#pragma unroll
+        for (int cg = 0; cg < NCG; ++cg) {
+          const float y00 = z0[16 * cg], y01 = z0[COP + 16 * cg];
+          const float y10 = z0[ZC * COP + 16 * cg], y11 = z0[ZC * COP + COP + 16 * cg];
+          const float r0 = ai0 * y00 + ai1 * y10, r1 = ai0 * y01 + ai1 * y11;  // row i of A dY
+          db[cg][0] = r0;
+          db[cg][1] = r0 + r1;
+          db[cg][2] = r0 - r1;
+          db[cg][3] = -r1;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+#pragma unroll
+            for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = mfma16(va[h][jj], db[cg][jj], acc[jj][h][cg]);
+      }
+    }
+  }
+  // inverse transform dW[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]; lane holds
+  // ci 16 h + 4 kq + rr (of the chunk), co 16 cg + tl
+  float* out = a.wpart + ((int64_t)r * a.splits + sp) * WPART;
+  gb_s[tid] = gb;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    __syncthreads();  // the last band's readers (or the previous chunk's) are done with smem
+    float* px = smem + wi * (3 * 16 * CO);
+#pragma unroll
+    for (int cg = 0; cg < NCG; ++cg)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float m0 = acc[0][h][cg][rr], m1 = acc[1][h][cg][rr], m2 = acc[2][h][cg][rr], m3 = acc[3][h][cg][rr];
+        const int o = (4 * kq + rr) * CO + 16 * cg + tl;
+        px[o] = (m0 + 0.5f * m1) + 0.5f * m2;
+        px[16 * CO + o] = 0.5f * m1 - 0.5f * m2;
+        px[32 * CO + o] = (0.5f * m1 + 0.5f * m2) + m3;
+      }
+    __syncthreads();
+    for (int e = tid; e < 16 * CO; e += 256) {  // (ci of the group, co)
+      const int ci = chn * CIB + 16 * h + e / CO, co = e % CO;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float p0 = smem[0 * 3 * 16 * CO + kx * 16 * CO + e], p1 = smem[1 * 3 * 16 * CO + kx * 16 * CO + e];
+        const float p2 = smem[2 * 3 * 16 * CO + kx * 16 * CO + e], p3 = smem[3 * 3 * 16 * CO + kx * 16 * CO + e];
+        out[a.off_w + ((0 * 3 + kx) * CI + ci) * CO + co] = (p0 + 0.5f * p1) + 0.5f * p2;
+        out[a.off_w + ((1 * 3 + kx) * CI + ci) * CO + co] = 0.5f * p1 - 0.5f * p2;
+        out[a.off_w + ((2 * 3 + kx) * CI + ci) * CO + co] = (0.5f * p1 + 0.5f * p2) + p3;
+      }
+    }
+  }
+  __syncthreads();
+  if (chn == 0 && tid < CO) {  // channel tid: quad tid / 4 of threads tid / 4 + (CO / 4) i, summed in thread order
+    constexpr int Z4 = CO / 4;
+    float s = 0.0f;
+    for (int i = 0; i < 256 / Z4; ++i) s += gb_s[tid / 4 + Z4 * i][tid % 4];
     out[a.off_b + tid] = s;
   }
 }
@@ -1086,16 +1570,18 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 // BR, NW> (wgrad); geometry checked by static_asserts, LDS per block in the comment
 // ------------------------------------------------------------------------------------------------
 #define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
-#define CONV2_FWD conv_kernel<32, 32, 32, 32, 0, 4, 4, 2, EPI_FWD_POOL>    /* 4 bands, 42.6 KB */
-#define CONV3_FWD conv_kernel<15, 15, 32, 64, 1, 16, 4, 2, EPI_FWD>        /* 1 band,  42.0 KB */
-#define CONV4_FWD conv_kernel<15, 15, 64, 64, 0, 6, 3, 2, EPI_FWD_POOL, 2>  /* 1 band,  29.1 KB */
-#define CONV4_DGRAD conv_kernel<13, 13, 64, 64, 2, 16, 4, 2, EPI_BWD_MASK, 2> /* 1 band, 42.0 KB */
-#define CONV3_DGRAD conv_kernel<15, 15, 64, 32, 1, 16, 4, 2, EPI_BWD_UNPOOL, 2> /* 1 band, 42.0 KB */
-#define CONV2_DGRAD conv_kernel<30, 30, 32, 32, 2, 16, 4, 4, EPI_BWD_MASK, 2> /* 2 bands, 42.0 KB */
+// Winograd F(2x2,3x3): <HI, WI, CI, CO, PAD, tile rows per band, EPI>; bands = ceil(tile rows / BTY)
+#define CONV2_FWD wino_kernel<32, 32, 32, 32, 0, 4, EPI_FWD_POOL>     /* 15x15 windows, 4 bands, 59.2 KB */
+#define CONV3_FWD wino_kernel<15, 15, 32, 64, 1, 8, EPI_FWD>          /* 8x8 tiles,    1 band,  59.7 KB */
+#define CONV4_FWD wino_kernel<15, 15, 64, 64, 0, 6, EPI_FWD_POOL>     /* 6x6 windows,  1 band,  67.9 KB */
+#define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK>   /* 8x8 tiles,    2 bands, 63.7 KB */
+#define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL> /* 8x8 tiles,    2 bands, 63.7 KB */
+#define CONV2_DGRAD wino_kernel<30, 30, 32, 32, 2, 4, EPI_BWD_MASK>   /* 16x16 tiles,  4 bands, 61.8 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
-#define CONV2_WGRAD wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 3, 3>
-#define CONV3_WGRAD wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 5, 3>
-#define CONV4_WGRAD wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 6, 3>
+// Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
+#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32>  /* 15x15 tiles, 5 bands, 56.9 KB */
+#define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 57.1 KB */
+#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32>  /* 6x6 tiles, 1 band, 2 ci chunks */
 
 inline int launch_status() {
   const hipError_t e = hipGetLastError();
@@ -1117,16 +1603,24 @@ ConvArgs conv_args(const float* in, int in_mode, int row_base, const int32_t* id
   return a;
 }
 
+// In-stream kernel timing (bench.py): prof = k > 0 records the event ev before / after launch k; prof =
+// MPLC_PROF_ALL records around every launch k, ev then pointing to an array of hipEvent_t indexed by k (1 .. 15).
+inline void cifar_prof_record(int prof, void* ev, int k, hipStream_t s) {
+  if (!ev) return;
+  if (prof == k) (void)hipEventRecord((hipEvent_t)ev, s);
+  else if (prof == MPLC_PROF_ALL) (void)hipEventRecord(static_cast<hipEvent_t*>(ev)[k], s);
+}
+
 // forward of conv1..dense5 for R models x B slots (train: dropout + codes; eval: inference)
 void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, int row_base, const int32_t* idx,
                      const int32_t* cnt, int cnt_all, const float* params, int64_t stride, const uint64_t* drop_key,
                      float* a1, float* d2, uint8_t* code2, float* a3, float* d4, uint8_t* code4, float* h5,
-                     uint8_t* code5, int prof, void* pb, void* pe, const float* glob = nullptr,
+                     uint8_t* code5, int prof, void* pb, void* pe, float* wu, const float* glob = nullptr,
                      const int32_t* w5src = nullptr) {
-#define PB(k) \
-  if (prof == (k) && pb) (void)hipEventRecord((hipEvent_t)pb, s)
-#define PE(k) \
-  if (prof == (k) && pe) (void)hipEventRecord((hipEvent_t)pe, s)
+#define PB(k) cifar_prof_record(prof, pb, (k), s)
+#define PE(k) cifar_prof_record(prof, pe, (k), s)
+  // conv2..conv4 weights in Winograd form (U = G g G^T per channel pair)
+  wino_u_kernel<0><<<dim3(7168 / 256, R), 256, 0, s>>>(params, stride, cnt, wu);
   ConvArgs c1 = conv_args(x, in_mode, row_base, idx, cnt, cnt_all, B, params + OFF_W1, stride);
   c1.bias = params + OFF_B1;
   c1.b_rstride = stride;
@@ -1134,7 +1628,7 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   PB(1);
   CONV1_FWD<<<dim3(4, B, R), 256, 0, s>>>(c1);
   PE(1);
-  ConvArgs c2 = conv_args(a1, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W2, stride);
+  ConvArgs c2 = conv_args(a1, 0, 0, nullptr, cnt, cnt_all, B, wu + WU_2, MPLC_CIFAR_WT);
   c2.bias = params + OFF_B2;
   c2.b_rstride = stride;
   c2.drop_key = drop_key;
@@ -1144,14 +1638,14 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   PB(2);
   CONV2_FWD<<<dim3(4, B, R), 256, 0, s>>>(c2);
   PE(2);
-  ConvArgs c3 = conv_args(d2, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W3, stride);
+  ConvArgs c3 = conv_args(d2, 0, 0, nullptr, cnt, cnt_all, B, wu + WU_3, MPLC_CIFAR_WT);
   c3.bias = params + OFF_B3;
   c3.b_rstride = stride;
   c3.out = a3;
   PB(3);
   CONV3_FWD<<<dim3(1, B, R), 256, 0, s>>>(c3);
   PE(3);
-  ConvArgs c4 = conv_args(a3, 0, 0, nullptr, cnt, cnt_all, B, params + OFF_W4, stride);
+  ConvArgs c4 = conv_args(a3, 0, 0, nullptr, cnt, cnt_all, B, wu + WU_4, MPLC_CIFAR_WT);
   c4.bias = params + OFF_B4;
   c4.b_rstride = stride;
   c4.drop_key = drop_key;
@@ -1159,7 +1653,7 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   c4.out = d4;
   c4.code_out = code4;
   PB(4);
-  CONV4_FWD<<<dim3(1, B, R), 192, 0, s>>>(c4);
+  CONV4_FWD<<<dim3(1, B, R), 256, 0, s>>>(c4);
   PE(4);
   PB(5);
   dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, glob,
@@ -1183,10 +1677,8 @@ int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, 
   return launch_status();
 }
 
-#define PROF_BEGIN(k) \
-  if (t->prof_kernel == (k) && t->prof_begin) (void)hipEventRecord((hipEvent_t)t->prof_begin, s)
-#define PROF_END(k) \
-  if (t->prof_kernel == (k) && t->prof_end) (void)hipEventRecord((hipEvent_t)t->prof_end, s)
+#define PROF_BEGIN(k) cifar_prof_record(t->prof_kernel, t->prof_begin, (k), s)
+#define PROF_END(k) cifar_prof_record(t->prof_kernel, t->prof_end, (k), s)
 
 int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   if (!t || t->n_rep < 1 || t->n_rep > 65535 || t->bmax < 1 || t->bmax > 65535) return MPLC_E_ARG;
@@ -1206,8 +1698,8 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                                                                    t->rep_glob, t->glob ? t->w5src : nullptr);
   const int32_t* w5src = t->glob ? t->w5src : nullptr;
   enqueue_forward(s, R, B, t->x, 1, 0, t->idx, t->cnt, 0, t->params, STRIDE, t->drop_key, t->a1, t->d2, t->code2,
-                  t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end, t->glob,
-                  w5src);
+                  t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end, t->wt,
+                  t->glob, w5src);
   PROF_BEGIN(6);
   head_kernel<<<R, 256, 0, s>>>(t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5,
                                 t->lr, t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
@@ -1217,37 +1709,38 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                                                             t->rms, t->glob, w5src, t->dz4, t->lr, t->rho,
                                                             t->one_minus_rho, t->decay, t->eps);
   PROF_END(7);
-  transpose_w_kernel<<<dim3(32, R), 256, 0, s>>>(t->params, t->cnt, t->wt);
+  // the data gradients' kernels (rotated, channels swapped) in Winograd form, over the forward's
+  wino_u_kernel<1><<<dim3(7168 / 256, R), 256, 0, s>>>(t->params, STRIDE, t->cnt, t->wt);
   const int SP = t->wg_splits;
   WgArgs w4{t->a3, 0, t->idx, t->cnt, B, SP, t->dz4, t->wpart, (int)OFF_W4, (int)OFF_B4};
   PROF_BEGIN(8);
-  CONV4_WGRAD<<<dim3(SP, R), 384, 0, s>>>(w4);
+  CONV4_WGRAD<<<dim3(SP, R, 2), 256, 0, s>>>(w4);
   PROF_END(8);
-  ConvArgs g4 = conv_args(t->dz4, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W4, MPLC_CIFAR_WT);
+  ConvArgs g4 = conv_args(t->dz4, 0, 0, nullptr, t->cnt, 0, B, t->wt + WU_4, MPLC_CIFAR_WT);
   g4.aux = t->a3;
   g4.out = t->dz3;
   PROF_BEGIN(9);
-  CONV4_DGRAD<<<dim3(1, B, R), 256, 0, s>>>(g4);
+  CONV4_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g4);
   PROF_END(9);
   WgArgs w3{t->d2, 0, t->idx, t->cnt, B, SP, t->dz3, t->wpart, (int)OFF_W3, (int)OFF_B3};
   PROF_BEGIN(10);
-  CONV3_WGRAD<<<dim3(SP, R), 192, 0, s>>>(w3);
+  CONV3_WGRAD<<<dim3(SP, R, 1), 256, 0, s>>>(w3);
   PROF_END(10);
-  ConvArgs g3 = conv_args(t->dz3, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W3, MPLC_CIFAR_WT);
+  ConvArgs g3 = conv_args(t->dz3, 0, 0, nullptr, t->cnt, 0, B, t->wt + WU_3, MPLC_CIFAR_WT);
   g3.code_in = t->code2;
   g3.out = t->dz2;
   PROF_BEGIN(11);
-  CONV3_DGRAD<<<dim3(1, B, R), 256, 0, s>>>(g3);
+  CONV3_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g3);
   PROF_END(11);
   WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2};
   PROF_BEGIN(12);
-  CONV2_WGRAD<<<dim3(SP, R), 192, 0, s>>>(w2);
+  CONV2_WGRAD<<<dim3(SP, R, 1), 256, 0, s>>>(w2);
   PROF_END(12);
-  ConvArgs g2 = conv_args(t->dz2, 0, 0, nullptr, t->cnt, 0, B, t->wt + WT_W2, MPLC_CIFAR_WT);
+  ConvArgs g2 = conv_args(t->dz2, 0, 0, nullptr, t->cnt, 0, B, t->wt + WU_2, MPLC_CIFAR_WT);
   g2.aux = t->a1;
   g2.out = t->dz1;
   PROF_BEGIN(13);
-  CONV2_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g2);
+  CONV2_DGRAD<<<dim3(4, B, R), 256, 0, s>>>(g2);
   PROF_END(13);
   WgArgs w1{t->x, 1, t->idx, t->cnt, B, SP, t->dz1, t->wpart, (int)OFF_W1, (int)OFF_B1};
   PROF_BEGIN(14);
@@ -1261,7 +1754,8 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
 }
 
 int64_t mplc_cifar_eval_workspace_floats(int n_models, int chunk) {
-  return (int64_t)n_models * chunk * (MPLC_CIFAR_A1 + MPLC_CIFAR_D2 + MPLC_CIFAR_A3 + MPLC_CIFAR_D4 + MPLC_CIFAR_H5);
+  return (int64_t)n_models * chunk * (MPLC_CIFAR_A1 + MPLC_CIFAR_D2 + MPLC_CIFAR_A3 + MPLC_CIFAR_D4 + MPLC_CIFAR_H5) +
+         (int64_t)n_models * MPLC_CIFAR_WT;
 }
 
 int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
@@ -1276,10 +1770,11 @@ int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const
   float* a3 = d2 + mc * MPLC_CIFAR_D2;
   float* d4 = a3 + mc * MPLC_CIFAR_A3;
   float* h5 = d4 + mc * MPLC_CIFAR_D4;
+  float* wu = h5 + mc * MPLC_CIFAR_H5;  // [n_models][MPLC_CIFAR_WT] conv2..conv4 in Winograd form
   for (int s0 = 0; s0 < n_samples; s0 += chunk) {
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
     enqueue_forward(s, n_models, chunk, x, 2, s0, nullptr, nullptr, cn, params, stride, nullptr, a1, d2, nullptr, a3,
-                    d4, nullptr, h5, nullptr, 0, nullptr, nullptr);
+                    d4, nullptr, h5, nullptr, 0, nullptr, nullptr, wu);
     eval_head_kernel<<<n_models, 256, 0, s>>>(h5, cn, chunk, labels, s0, params, stride, correct, loss_sum);
     const int st = launch_status();
     if (st) return st;

@@ -45,6 +45,14 @@ constexpr int64_t OFF_W1 = MPLC_CNN_OFF_W1, OFF_B1 = MPLC_CNN_OFF_B1, OFF_W2 = M
 constexpr int ADAM_LAST = 1 << 30;  // adam_t flag: the optimizer's last step
 constexpr int A1P = 33;  // padded channel stride of conv1 output tiles in LDS (bank-conflict-free A reads)
 
+// Register cap of the three convolution kernels (build experiments: -DCONV_VGPR_CAP=N leaves 512 - 2N registers
+// per SIMD lane beside two convolution waves, room for a wave of another kernel)
+#ifdef CONV_VGPR_CAP
+#define CONV_REGS __attribute__((amdgpu_num_vgpr(CONV_VGPR_CAP)))
+#else
+#define CONV_REGS
+#endif
+
 // Cross-lane add within rows of 16 lanes on DPP (VALU, no LDS round trip).  Each level adds the partner's
 // value exactly as `d += __shfl_xor(d, m)` does (commutative adds of the same operands: bit-identical).
 template <int CTRL>
@@ -240,7 +248,7 @@ __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_fwd_kernel(
+__global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, const float* __restrict__ U,
     float* __restrict__ pooled, uint8_t* __restrict__ code) {
@@ -819,7 +827,7 @@ constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quart
 static_assert(BWD_BANDS * BWD_BAND_TILES >= BWD_TILES && (BWD_BANDS - 1) * BWD_BAND_TILES < BWD_TILES,
               "MPLC_CNN_W1_BANDS must be ceil(169 / 64)");
 
-__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_bwd_data_kernel(
+__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_bwd_data_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     const float* __restrict__ params, int64_t stride, const float* __restrict__ Ur,
     const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
@@ -1068,7 +1076,7 @@ constexpr int WG_A1 = 6 * A1 * WG_CS;             // one band's conv1 rows [6][2
 constexpr int WG_VS = 80;                         // window stride of the staged (value, argmax) pairs (int2)
 constexpr int WG_PX = 3 * 16 * C2 + 16;           // one wave's P_i for one ci half: [3][16 ci][64 co] (+pad)
 
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_kernel(
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_wgrad_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
     int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
     const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
@@ -1390,10 +1398,13 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
     return MPLC_E_ARG;
   if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
   if (t->glob && (!t->rep_glob || !t->w3src)) return MPLC_E_ARG;
+  if (t->phases & ~(MPLC_PHASE_FRONT | MPLC_PHASE_DENSE | MPLC_PHASE_BACK)) return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int R = t->n_rep, B = t->bmax;
   const int64_t S = MPLC_CNN_STRIDE;
   const int64_t slots = (int64_t)R * B;
+  const int ph = t->phases ? t->phases : (MPLC_PHASE_FRONT | MPLC_PHASE_DENSE | MPLC_PHASE_BACK);
+  if (ph & MPLC_PHASE_FRONT) {
   schedule_kernel<<<(unsigned)((slots + 255) / 256), 256, 0, s>>>(t->reps, R, B, t->rows, t->splits, t->seq, t->step,
                                                                    t->minibatch_count, t->round_len, t->epochs,
                                                                    t->idx, t->cnt, t->adam_t, t->rep_glob,
@@ -1404,8 +1415,10 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->w2t,
                                                          t->pooled, t->code);
   PROF_END(1);
-  PROF_BEGIN(2);
+  }
   const int32_t* w3src = t->glob ? t->w3src : nullptr;
+  if (ph & MPLC_PHASE_DENSE) {
+  PROF_BEGIN(2);
   dense_fwd_kernel<<<dim3((B + 31) / 32, R), 256, 0, s>>>(t->pooled, (int64_t)B * FEAT, t->cnt, 0, B, t->params, S,
                                                           t->glob, w3src, t->hidden);
   PROF_END(2);
@@ -1419,6 +1432,8 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                                   w3src, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
   PROF_END(4);
+  }
+  if (ph & MPLC_PHASE_BACK) {
   winograd_w2r_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(5);
   conv_bwd_data_kernel<<<dim3(BWD_BANDS, B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
@@ -1433,6 +1448,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                                  t->w2_part, t->params, t->adam_m, t->adam_v, S,
                                                                  t->lr, t->beta1, t->beta2, t->eps);
   PROF_END(7);
+  }
   return launch_status();
 }
 

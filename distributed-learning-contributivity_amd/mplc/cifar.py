@@ -18,18 +18,28 @@ NPARAM = 1250954
 WG_SAMPLES = 2
 A1, D2, A3, D4, H5 = 32768, 7200, 14400, 2304, 512
 DZ4, DZ3, DZ2, DZ1 = 10816, 14400, 28800, 32768
-WT, WPART = 64512, 65664
+WT, WPART = 114688, 65664  # MPLC_CIFAR_WT: conv2..conv4 in Winograd form
 EVAL_FLOATS = A1 + D2 + A3 + D4 + H5  # per model per evaluated sample
 
 KERNEL_IDS = {"conv1_fwd": 1, "conv2_fwd": 2, "conv3_fwd": 3, "conv4_fwd": 4, "dense5_fwd": 5, "head": 6,
               "dense5_bwd": 7, "conv4_wgrad": 8, "conv4_dgrad": 9, "conv3_wgrad": 10, "conv3_dgrad": 11,
               "conv2_wgrad": 12, "conv2_dgrad": 13, "conv1_wgrad": 14, "rmsprop_small": 15}
-# algorithmic FLOPs per sample of each profiled launch (bench roofline)
-FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 900 * 32 * 288 * 2, "conv3_fwd": 225 * 64 * 288 * 2,
-                   "conv4_fwd": 144 * 64 * 576 * 2, "conv4_dgrad": 144 * 64 * 576 * 2,
-                   "conv3_dgrad": 225 * 32 * 576 * 2, "conv2_dgrad": 900 * 32 * 288 * 2,
-                   "conv4_wgrad": 144 * 64 * 576 * 2, "conv3_wgrad": 225 * 64 * 288 * 2,
-                   "conv2_wgrad": 900 * 32 * 288 * 2, "conv1_wgrad": 1024 * 32 * 27 * 2}
+# algorithmic FLOPs per sample of each profiled launch (bench roofline): what the kernel's algorithm executes.
+# conv2..conv4 run in Winograd form F(2x2,3x3) / F(3x3,2x2): (2x2 output tiles) x 16 transform points x CI x CO
+# multiply-adds; conv1 is a direct implicit GEMM.  DIRECT_FLOP_PER_SAMPLE: the direct convolution's count (the
+# reference's arithmetic), 2.25x the Winograd count, reported beside it as the equivalent rate.
+FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 225 * 16 * 32 * 32 * 2,
+                   "conv3_fwd": 64 * 16 * 32 * 64 * 2, "conv4_fwd": 36 * 16 * 64 * 64 * 2,
+                   "conv4_dgrad": 64 * 16 * 64 * 64 * 2, "conv3_dgrad": 64 * 16 * 64 * 32 * 2,
+                   "conv2_dgrad": 256 * 16 * 32 * 32 * 2, "conv4_wgrad": 36 * 16 * 64 * 64 * 2,
+                   "conv3_wgrad": 64 * 16 * 32 * 64 * 2, "conv2_wgrad": 225 * 16 * 32 * 32 * 2,
+                   "conv1_wgrad": 1024 * 32 * 27 * 2}
+DIRECT_FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 900 * 32 * 288 * 2,
+                          "conv3_fwd": 225 * 64 * 288 * 2, "conv4_fwd": 144 * 64 * 576 * 2,
+                          "conv4_dgrad": 144 * 64 * 576 * 2, "conv3_dgrad": 225 * 32 * 576 * 2,
+                          "conv2_dgrad": 900 * 32 * 288 * 2, "conv4_wgrad": 144 * 64 * 576 * 2,
+                          "conv3_wgrad": 225 * 64 * 288 * 2, "conv2_wgrad": 900 * 32 * 288 * 2,
+                          "conv1_wgrad": 1024 * 32 * 27 * 2}
 
 
 class CifarTrainT(ctypes.Structure):
@@ -129,10 +139,43 @@ class CifarModel:
     def step(self, st, s, prof):
         st.t.step = s
         if prof is not None:
+            if prof.all:
+                prof.bind(self.KERNEL_IDS)
             ev0, ev1 = prof.pair()
-            st.t.prof_kernel = self.KERNEL_IDS[prof.kernel]
+            st.t.prof_kernel = -1 if prof.all else self.KERNEL_IDS[prof.kernel]  # -1: MPLC_PROF_ALL
             st.t.prof_begin, st.t.prof_end = ev0, ev1
+        else:
+            st.t.prof_kernel, st.t.prof_begin, st.t.prof_end = 0, None, None
         _native.check(self.lib.mplc_cifar_train_step(ctypes.byref(st.t), st.stream), "mplc_cifar_train_step")
+        if prof is not None and prof.want_stash:
+            prof.stash_step(st.ws["cnt"], st.ws["opt_t"], st.ws["w5src"])
+
+    @staticmethod
+    def algorithmic_units(stash):
+        """Algorithmic work of the timed steps from their stashed schedules [(cnt, opt_t, w5src)]: samples (the
+        convolutions' unit) and the HBM bytes of the two W5 kernels (csrc/cifar_cnn.hip):
+          dense5_fwd: W5 read; per sample the d4 row read, the h5 row written with its code byte;
+          dense5_bwd: W5 read and written, the RMSprop accumulator written (and read unless the optimizer is
+                      fresh, t = 1); per sample d4, its code byte and dh5 read, the un-pooled dz4 written (4
+                      window pixels per pooled element).
+        A FedAvg round's first step reads W5 from the coalition row (w5src >= 0), shared by the coalition's
+        replicas: counted once per coalition."""
+        import torch
+        w5 = float(D4 * H5 * 4)
+        samples = d5b = d5f = 0.0
+        for cnt, at, src in stash:
+            cnt = cnt.to(torch.float64)
+            act = (cnt > 0).to(torch.float64)
+            shared = src >= 0
+            n_shared_rows = float(torch.unique(src[shared & (cnt > 0)]).numel())
+            own = (~shared).to(torch.float64)
+            acc_rd = (at > 1).to(torch.float64)
+            d5b += float((act * (w5 * (own + 2.0 + acc_rd)) + cnt * float(D4 * 4 + D4 + H5 * 4 + 4 * D4 * 4)).sum())
+            d5f += float((act * w5 * own + cnt * float(D4 * 4 + H5 * 4 + H5)).sum())
+            d5b += n_shared_rows * w5
+            d5f += n_shared_rows * w5
+            samples += float(cnt.sum())
+        return {"samples": samples, "dense5_bwd_bytes": d5b, "dense5_fwd_bytes": d5f}
 
     def evaluate(self, eng, sel, x, y):
         import torch

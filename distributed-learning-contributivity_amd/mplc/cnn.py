@@ -76,7 +76,7 @@ class TrainT(ctypes.Structure):
                 ("dhidden", ctypes.c_void_p), ("dpooled", ctypes.c_void_p), ("w1_part", ctypes.c_void_p),
                 ("w2_part", ctypes.c_void_p), ("w2t", ctypes.c_void_p),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
-                ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("pad1", ctypes.c_int32),
+                ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("phases", ctypes.c_int32),
                 ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p), ("hstats", ctypes.c_void_p),
                 ("glob", ctypes.c_void_p), ("rep_glob", ctypes.c_void_p), ("w3src", ctypes.c_void_p)]
 
@@ -545,7 +545,12 @@ class CnnBatchTrainer:
                for ci in range(C) if st.coal_is_single[ci]}
         per_epoch_fed = eng.minibatch_count * st.round_len
         progress = getattr(eng, "progress", None)
+        stats = eng.stats
         for s in range(st.total_steps):
+            # replica-steps launched, and those of replicas still training (early stopping leaves the stopped
+            # coalitions' replicas idle in the lockstep batch until it ends)
+            stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
+            stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(np.sum(st.kind_host != REP_IDLE))
             if progress is not None and s % 30 == 0:
                 progress(s, st.total_steps, st.R)
             if rec is not None and st.fed_steps and s % st.round_len == 0 and s < st.fed_steps:
@@ -602,7 +607,12 @@ class CnnBatchTrainer:
         return self.eng.model_impl.evaluate(self.eng, sel, x, y)
 
     def _val_loss(self, params, rows):
-        _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)
+        import time
+        t0 = time.perf_counter()
+        _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)  # synchronises (host copy)
+        st = self.eng.stats
+        st["es_val_s"] = st.get("es_val_s", 0.0) + time.perf_counter() - t0
+        st["es_val_evals"] = st.get("es_val_evals", 0) + len(rows)
         return [float(v) for v in loss]
 
 

@@ -213,6 +213,7 @@ class CoalitionEngine:
             self.stats["samples"] += int(sum(int(ep) * sum(self.partner_sizes[p] for p in c)
                                              for c, ep in zip(coal, e)))
         self.stats["coalitions"] += len(coalitions)
+        self.last_epochs_done = epochs_done  # realised epochs of this call's coalitions (early stopping)
         if return_details:
             # es_val_loss: the val losses the early-stopping rule compared (start-of-epoch global model for
             # FedAvg, end-of-epoch model for singletons); empty when early stopping is inactive

@@ -58,7 +58,8 @@ extern "C" {
 #define MPLC_CIFAR_DZ3 14400         /* conv3 pre-activation gradient 15x15x64    */
 #define MPLC_CIFAR_DZ2 28800         /* conv2 pre-activation gradient 30x30x32    */
 #define MPLC_CIFAR_DZ1 32768         /* conv1 pre-activation gradient 32x32x32    */
-#define MPLC_CIFAR_WT 64512          /* flipped/transposed W2|W3|W4 for the data gradients */
+#define MPLC_CIFAR_WT 114688         /* W2|W3|W4 in Winograd form (16 x ci x co each): the forward's, then
+                                        the data gradients' (rotated, channels swapped) */
 #define MPLC_CIFAR_WPART 65664       /* partial gradient row of W1..b4 (= params layout prefix) */
 #ifndef MPLC_CIFAR_WG_SAMPLES
 #define MPLC_CIFAR_WG_SAMPLES 2      /* samples per weight-gradient split (fixed: reproducible sums) */
@@ -103,13 +104,14 @@ typedef struct {
   float* dz3;             /* [.][MPLC_CIFAR_DZ3]                                          */
   float* dz2;             /* [.][MPLC_CIFAR_DZ2]                                          */
   float* dz1;             /* [.][MPLC_CIFAR_DZ1]                                          */
-  float* wt;              /* [n_rep][MPLC_CIFAR_WT]                                       */
+  float* wt;              /* [n_rep][MPLC_CIFAR_WT] Winograd-form conv weights (workspace)  */
   float* wpart;           /* [n_rep][wg_splits][MPLC_CIFAR_WPART]                         */
   /* optimizer (Keras 2.3.1 RMSprop).  one_minus_rho is passed separately: Keras computes (1. - rho) on
    * the Python double (rho is not a backend variable) and rounds once, fp32(1 - 0.9) = 0.1f, which is
    * not 1 - fp32(0.9). */
   float lr, rho, one_minus_rho, decay, eps;
-  /* optional in-stream timing of one launch of the step (bench roofline); ids in mplc/cifar.py */
+  /* optional in-stream timing of one launch of the step (bench roofline); ids in mplc/cifar.py.  prof_kernel =
+   * MPLC_PROF_ALL times every launch k = 1 .. 15, prof_begin / prof_end then pointing to hipEvent_t arrays of 16 */
   int32_t prof_kernel;
   void* prof_begin;
   void* prof_end;

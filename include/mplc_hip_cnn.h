@@ -45,6 +45,9 @@ extern "C" {
 #define MPLC_CNN_STRIDE 1199936    /* row stride, multiple of 64 floats */
 #define MPLC_PROF_ALL (-1)         /* mplc_cnn_train_t.prof_kernel: time every launch of the step */
 #define MPLC_PROF_KERNELS 7
+#define MPLC_PHASE_FRONT 1
+#define MPLC_PHASE_DENSE 2
+#define MPLC_PHASE_BACK 4
 #define MPLC_CNN_W1_BANDS 3        /* data-gradient blocks per sample (64 Winograd tiles each) */
 #define MPLC_CNN_W2T 32768         /* per-model W2 workspace: 16 Winograd planes x 32 x 64 floats */
 #define MPLC_CNN_FEAT 9216         /* flattened pooled features */
@@ -119,7 +122,12 @@ typedef struct {
    * every launch k is timed, prof_begin / prof_end then point to hipEvent_t arrays of MPLC_PROF_KERNELS + 1
    * entries indexed by k */
   int32_t prof_kernel;
-  int32_t pad1;
+  /* Which launches of the step to issue (bit mask; 0 = all, the whole step): MPLC_PHASE_FRONT = schedule,
+   * W2 Winograd form, conv_fwd; MPLC_PHASE_DENSE = dense_fwd, head, dense1_bwd_adam; MPLC_PHASE_BACK = the
+   * rotated W2, conv_bwd_data, conv_wgrad, adam_small.  Issuing the phases of one step separately, in order,
+   * on one stream is the same computation; the host may interleave the phases of two replica ranges on two
+   * streams (MFMA-bound convolutions beside the HBM-bound dense layer). */
+  int32_t phases;
   void* prof_begin;
   void* prof_end;
   /* optional training history (NULL = off): per replica, the step's [sum of per-sample CE before the

@@ -241,3 +241,27 @@ def test_empty_minibatch_partner_restarts_from_global_model():
     assert np.array_equal(skip["scores"], full["scores"])
     for a, b in zip(skip["models"][0], full["models"][0]):
         assert np.array_equal(a, b)
+
+
+def test_all_kernel_timer_is_result_neutral(engine):
+    """bench.py's config #4 line times every launch of the CIFAR step in stream (prof_kernel = MPLC_PROF_ALL, event
+    arrays): v(S) unchanged, every kernel timed once per step, the stashed schedules count every sample."""
+    from mplc.cifar import KERNEL_IDS, CifarModel
+    from mplc.profiling import KernelTimer
+    coals = [(0,), (1, 2), (0, 1, 2)]
+    timer = KernelTimer("all", list(KERNEL_IDS), stash=True)
+    engine.profiler = timer
+    try:
+        timed = engine.evaluate(coals)
+    finally:
+        engine.profiler = None
+    plain = engine.evaluate(coals)
+    assert np.array_equal(timed, plain)
+    steps = len(timer.stash)
+    assert steps > 0
+    for k in KERNEL_IDS:
+        assert timer.launches(k) == steps and timer.total_ms(k) > 0.0, k
+    units = CifarModel.algorithmic_units(timer.stash)
+    sizes = engine.partner_sizes
+    assert units["samples"] == engine.epoch_count * sum(sizes[p] for c in coals for p in c)
+    assert units["dense5_bwd_bytes"] > units["dense5_fwd_bytes"] > 0
