@@ -900,6 +900,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll 1
   for (int q = 0; q < 4; ++q) {  // channel quarters
     __syncthreads();             // previous quarter's readers done (and the zero columns / image written)
+#ifndef BWD_EXP_NOSTAGE  // timing experiment switch (garbage results): the quarter's staging compiled out
     {
       constexpr int UIT = BWD_UQ / 4 / BWD_THREADS;  // 8 chunks of 4 floats per thread
       fvec4 uv[UIT];  // the quarter's Ur: loads in flight while the band is un-pooled
@@ -927,6 +928,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
         ur_s[pair * 4 + (m ^ ((pair >> 2) & 3))] = uv[s];
       }
     }
+#endif
     if (q < 3) fetch(q + 1);
     __syncthreads();
     if (active) {
@@ -960,10 +962,17 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           v[4 * i + 2] = t[i][2] - t[i][1];
           v[4 * i + 3] = t[i][1] - t[i][3];
         }
+#ifndef BWD_EXP_NOMFMA
 #pragma unroll
         for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
           for (int h = 0; h < 2; ++h) acc[xi][h] = mfma16(v[xi], b[h][xi >> 2][xi & 3], acc[xi][h]);
+#else  // timing experiment: operands formed and consumed by VALU adds instead of the MFMAs
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[xi][h][0] += v[xi] + b[h][xi >> 2][xi & 3];
+#endif
       }
     }
   }
@@ -979,7 +988,15 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     }
   fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
   fvec4 gacc1 = gacc;
+#ifdef BWD_EXP_NOEPI  // timing experiment: the epilogue compiled out (the accumulators still consumed)
   if (active) {
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) gacc += acc[xi][0] + acc[xi][1];
+  }
+  if (false) {
+#else
+  if (active) {
+#endif
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       // positions of the MFMA rows m = 4 kq' + q: tile 4kq' + rr of the group, window pixel q = 2a + b

@@ -608,6 +608,10 @@ class CnnBatchTrainer:
 
     def _val_loss(self, params, rows):
         import time
+        import torch
+        # the stats time the evaluation itself: the training steps the host queued ahead finish first (the
+        # loss's host copy below synchronises anyway, so this wait costs no throughput)
+        torch.cuda.synchronize(self.eng.device)
         t0 = time.perf_counter()
         _, loss = self._evaluate(params, rows, self.eng.x_val_d, self.eng.y_val_d)  # synchronises (host copy)
         st = self.eng.stats
