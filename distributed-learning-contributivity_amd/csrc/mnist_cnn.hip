@@ -904,8 +904,11 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     {
       constexpr int UIT = BWD_UQ / 4 / BWD_THREADS;  // 8 chunks of 4 floats per thread
       fvec4 uv[UIT];  // the quarter's Ur: loads in flight while the band is un-pooled
+#if !defined(BWD_EXP_NOSTAGE_UR)
 #pragma unroll
       for (int s = 0; s < UIT; ++s) uv[s] = Uq[q * (BWD_UQ / 4) + tid + BWD_THREADS * s];
+#endif
+#ifndef BWD_EXP_NOSTAGE_DZ
 #pragma unroll
       for (int s = 0; s < BWD_PRE; ++s) {  // un-pool the quarter's (dp, code) into the dense band
         const int e = tid + BWD_THREADS * s;
@@ -921,12 +924,15 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           d[BWD_DC * BWD_CS + BWD_CS] = (sel == 3) ? v : 0.0f;
         }
       }
+#endif
+#ifndef BWD_EXP_NOSTAGE_UR
 #pragma unroll
       for (int s = 0; s < UIT; ++s) {  // chunk k = (co, ci, m): stored at m ^ ((ci >> 2) & 3)
         const int k = tid + BWD_THREADS * s;
         const int pair = k >> 2, m = k & 3;
         ur_s[pair * 4 + (m ^ ((pair >> 2) & 3))] = uv[s];
       }
+#endif
     }
 #endif
     if (q < 3) fetch(q + 1);
