@@ -943,6 +943,183 @@ void wgrad_kernel(const WgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Wave-local variant of wino_kernel for the CO = 32 layers (conv2 forward, conv2 and conv3 data gradients):
+// each wave owns one 16-tile group and ALL 16 transform points for the 32 output channels (2 x 16 accumulators
+// of 16x16x4), so the output transform and the epilogue stay in registers (no LDS round trip, no barrier after
+// the staging).  Per k-step (4 input channels) a lane reads its tile's 4x4 patch (16 LDS values), forms the 16
+// values of V with 32 adds and issues 32 MFMAs with U from L2 (32 B operands, loaded one k-step ahead):
+// half the LDS reads and 2/3 of the VALU per MFMA of the row-per-wave form at CO = 32 (which issues 8 MFMAs
+// per 8 reads and 12 adds).  NW waves per block = the band's 16-tile groups.
+// ------------------------------------------------------------------------------------------------
+template <int HI, int WI, int CI, int CO, int PAD, int BTY, int NW, int EPI>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wl_kernel(const ConvArgs a) {
+  constexpr bool POOL = (EPI == EPI_FWD_POOL);
+  constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
+  constexpr int PH = HO / 2, PW = WO / 2;
+  constexpr int TYT = POOL ? PH : (HO + 1) / 2;
+  constexpr int TXT = POOL ? PW : (WO + 1) / 2;
+  constexpr int LR = 2 * BTY + 2, LC = 2 * TXT + 2;
+  constexpr int CIP = CI + 1;
+  constexpr int ROWP = LC * CIP;
+  constexpr int NK = CI / 4;
+  constexpr int NTHR = NW * 64;
+  static_assert(CO == 32 && CI % 8 == 0, "wave-local form: 32 output channels");
+  static_assert(NW * 16 >= BTY * TXT, "one 16-tile group per wave");
+  __shared__ float in_s[LR * ROWP];
+  const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+  const int count = a.cnt ? a.cnt[r] : a.cnt_all;
+  if (j >= count) return;
+  const int tid = threadIdx.x;
+  const int64_t slot = (int64_t)r * a.bmax + j;
+  constexpr int IN_SZ = HI * WI * CI;
+  const float* src = a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ : a.in + slot * IN_SZ;
+  const int ty0 = band * BTY;
+  const int bty = min(BTY, TYT - ty0);
+  const int ntile = bty * TXT;
+  {
+    constexpr int C4 = CI / 4;
+    constexpr int TOT = LR * LC * C4;
+    constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+    fvec4 v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e4 = tid + k * NTHR;
+      const int pix = e4 / C4, c4 = e4 % C4;
+      const int iy = 2 * ty0 - PAD + pix / LC, ix = pix % LC - PAD;
+      const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+      const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? src + (iy * WI + ix) * CI + 4 * c4 : src);
+      v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e4 = tid + k * NTHR;
+      if (e4 < TOT) {
+        float* d = in_s + e4 / C4 * CIP + 4 * (e4 % C4);
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  if (16 * wave >= ntile) return;  // wave-uniform; no barrier follows
+  const int tl = lane & 15, kq = lane >> 4;
+  const int tile = min(16 * wave + tl, ntile - 1);
+  const float* dpa = in_s + ((2 * (tile / TXT)) * LC + 2 * (tile % TXT)) * CIP + kq;
+  // B operands of k-step st: U[xi][4 st + kq][16 cg + tl], 16 xi x 2 cg
+  const float* Ub = a.w + (int64_t)r * a.w_rstride + kq * CO + tl;
+  auto load_b = [&](int st, float (&bv)[32]) {
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+      for (int cg = 0; cg < 2; ++cg) bv[2 * xi + cg] = Ub[(int64_t)xi * CI * CO + (4 * st) * CO + 16 * cg];
+  };
+  fvec4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) acc[xi][0] = acc[xi][1] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto kstep = [&](int st, const float (&bv)[32]) {
+    const float* d0 = dpa + 4 * st;
+    float t[4][4];  // t[i][c] = (B^T d)[i][c]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float d_0 = d0[c * CIP], d_1 = d0[ROWP + c * CIP], d_2 = d0[2 * ROWP + c * CIP], d_3 = d0[3 * ROWP + c * CIP];
+      t[0][c] = d_0 - d_2;
+      t[1][c] = d_1 + d_2;
+      t[2][c] = d_2 - d_1;
+      t[3][c] = d_1 - d_3;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v0 = t[i][0] - t[i][2], v1 = t[i][1] + t[i][2], v2 = t[i][2] - t[i][1], v3 = t[i][1] - t[i][3];
+#pragma unroll
+      for (int cg = 0; cg < 2; ++cg) {
+        acc[4 * i + 0][cg] = mfma16(v0, bv[2 * (4 * i + 0) + cg], acc[4 * i + 0][cg]);
+        acc[4 * i + 1][cg] = mfma16(v1, bv[2 * (4 * i + 1) + cg], acc[4 * i + 1][cg]);
+        acc[4 * i + 2][cg] = mfma16(v2, bv[2 * (4 * i + 2) + cg], acc[4 * i + 2][cg]);
+        acc[4 * i + 3][cg] = mfma16(v3, bv[2 * (4 * i + 3) + cg], acc[4 * i + 3][cg]);
+      }
+    }
+  };
+  float b0[32], b1[32];
+  load_b(0, b0);
+#pragma unroll 1
+  for (int st = 0; st < NK; st += 2) {
+    load_b(st + 1, b1);
+    kstep(st, b0);
+    if (st + 2 < NK) load_b(st + 2, b0);
+    kstep(st + 1, b1);
+  }
+  // output transform in registers: lane holds M[xi][tile 4 kq + rr][co 16 cg + tl]
+  float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
+  const uint32_t rseed = (POOL && a.drop_key) ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int tt = 16 * wave + 4 * kq + rr;
+    if (tt >= ntile) continue;
+    const int ty = ty0 + tt / TXT, tx2 = tt % TXT;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+      const int co = 16 * cg + tl;
+      float tv[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float m0 = acc[4 * i][cg][rr], m1 = acc[4 * i + 1][cg][rr], m2 = acc[4 * i + 2][cg][rr],
+                    m3 = acc[4 * i + 3][cg][rr];
+        tv[i][0] = (m0 + m1) + m2;
+        tv[i][1] = (m1 - m2) - m3;
+      }
+      float y[4];
+      y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
+      y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
+      y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
+      y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
+      if constexpr (POOL) {
+        const float bv = a.bias[(int64_t)r * a.b_rstride + co];
+        float best = y[0] + bv;
+        int arg = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          const float z = y[q] + bv;
+          if (z > best) { best = z; arg = q; }
+        }
+        const int pidx = (ty * PW + tx2) * CO + co;
+        const float av = fmaxf(best, 0.0f);
+        if (a.drop_key) {
+          const bool keep = drop_keep(rseed, (uint32_t)pidx, THR_25);
+          o[pidx] = keep ? av * SCALE_25 : 0.0f;
+          a.code_out[slot * (PH * PW * CO) + pidx] =
+              (uint8_t)(arg | (keep ? CODE_KEEP : 0) | (best > 0.0f ? CODE_POS : 0));
+        } else {
+          o[pidx] = av;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int yy = 2 * ty + (q >> 1), xx = 2 * tx2 + (q & 1);
+          if (yy >= HO || xx >= WO) continue;
+          const int o_i = (yy * WO + xx) * CO + co;
+          if constexpr (EPI == EPI_BWD_MASK) {
+            o[o_i] = a.aux[slot * (HO * WO * CO) + o_i] > 0.0f ? y[q] : 0.0f;
+          } else if constexpr (EPI == EPI_BWD_UNPOOL) {
+            const uint32_t c = a.code_in[slot * (HO * WO * CO) + o_i];
+            const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
+            const bool pos = (c & CODE_POS) != 0;
+            const int sel = c & 3;
+#pragma unroll
+            for (int p4 = 0; p4 < 4; ++p4)
+              o[((2 * yy + (p4 >> 1)) * (2 * WO) + 2 * xx + (p4 & 1)) * CO + co] = (pos && sel == p4) ? dv : 0.0f;
+          } else {
+            o[o_i] = fmaxf(y[q] + a.bias[(int64_t)r * a.b_rstride + co], 0.0f);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Weight gradient of conv2..conv4 in Winograd form F(3x3, 2x2) (the transposed dual of the forward's
 // F(2x2, 3x3)): with Y = A^T [U (.) V] A per 2x2 output tile, dL/dU = (A dY A^T) (.) V, so
 //   dW[3x3] = G^T [ sum_tiles (A dY A^T) (.) (B^T d B) ] G
@@ -1571,12 +1748,20 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------------
 #define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
 // Winograd F(2x2,3x3): <HI, WI, CI, CO, PAD, tile rows per band, EPI>; bands = ceil(tile rows / BTY)
+#ifdef CIFAR_WINO_ROWS  // build switch: the row-per-wave form for the CO = 32 layers too (A/B)
 #define CONV2_FWD wino_kernel<32, 32, 32, 32, 0, 4, EPI_FWD_POOL>     /* 15x15 windows, 4 bands, 59.2 KB */
+#define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL> /* 8x8 tiles,    2 bands, 63.7 KB */
+#define CONV2_DGRAD wino_kernel<30, 30, 32, 32, 2, 4, EPI_BWD_MASK>   /* 16x16 tiles,  4 bands, 61.8 KB */
+#define CONV3_DGRAD_NT 256
+#else  // wave-local form: <HI, WI, CI, CO, PAD, BTY, waves, EPI>
+#define CONV2_FWD wino_wl_kernel<32, 32, 32, 32, 0, 4, 4, EPI_FWD_POOL>      /* 60 tiles, 4 bands, 42 KB */
+#define CONV3_DGRAD wino_wl_kernel<15, 15, 64, 32, 1, 4, 2, EPI_BWD_UNPOOL>  /* 32 tiles, 2 bands, 46.8 KB */
+#define CONV2_DGRAD wino_wl_kernel<30, 30, 32, 32, 2, 4, 4, EPI_BWD_MASK>    /* 64 tiles, 4 bands, 44.9 KB */
+#define CONV3_DGRAD_NT 128
+#endif
 #define CONV3_FWD wino_kernel<15, 15, 32, 64, 1, 8, EPI_FWD>          /* 8x8 tiles,    1 band,  59.7 KB */
 #define CONV4_FWD wino_kernel<15, 15, 64, 64, 0, 6, EPI_FWD_POOL>     /* 6x6 windows,  1 band,  67.9 KB */
 #define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK>   /* 8x8 tiles,    2 bands, 63.7 KB */
-#define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL> /* 8x8 tiles,    2 bands, 63.7 KB */
-#define CONV2_DGRAD wino_kernel<30, 30, 32, 32, 2, 4, EPI_BWD_MASK>   /* 16x16 tiles,  4 bands, 61.8 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 // Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
 #define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32>  /* 15x15 tiles, 5 bands, 56.9 KB */
@@ -1730,7 +1915,7 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   g3.code_in = t->code2;
   g3.out = t->dz2;
   PROF_BEGIN(11);
-  CONV3_DGRAD<<<dim3(2, B, R), 256, 0, s>>>(g3);
+  CONV3_DGRAD<<<dim3(2, B, R), CONV3_DGRAD_NT, 0, s>>>(g3);
   PROF_END(11);
   WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2};
   PROF_BEGIN(12);
