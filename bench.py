@@ -508,6 +508,7 @@ def bench_train(args, rank, world):
             reps0[0] = eng.stats["replicas"]
         on = not args.no_kernel_timer and (i < max(1, (planned + 1) // 2))
         eng.profiler = timer if on else None
+        eng.time_test_eval = on  # the test evaluation's time, on the timer-on sweeps (one sync per batch)
         n_on[0] += int(on)
         return one_step()
 
@@ -532,6 +533,7 @@ def bench_train(args, rank, world):
         total_train_samples = sum_over_ranks(samples, world)
     on_ms, off_ms = per_step[:n_on[0]], per_step[n_on[0]:]
     timer_note = {"steps_with_kernel_timer": n_on[0],
+                  "test_eval_ms_per_step": round(1000 * eng.stats.get("test_eval_s", 0.0) / max(1, n_on[0]), 1),
                   "ms_per_step_timer_on": round(1000 * sum(on_ms) / len(on_ms), 1) if on_ms else None,
                   "ms_per_step_timer_off": round(1000 * sum(off_ms) / len(off_ms), 1) if off_ms else None,
                   "note": "value covers every timed step; the kernels table and roofline come from the timer-on steps"}

@@ -597,7 +597,14 @@ class CnnBatchTrainer:
         glob = st.finalize()
         self.last_es_trace = val_hist
         self.last_models = glob.cpu().numpy() if keep_models else None
+        if getattr(eng, "time_test_eval", False):  # bench accounting: the test evaluation's own time
+            import time
+            import torch
+            torch.cuda.synchronize(eng.device)
+            t0 = time.perf_counter()
         correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
+        if getattr(eng, "time_test_eval", False):
+            eng.stats["test_eval_s"] = eng.stats.get("test_eval_s", 0.0) + time.perf_counter() - t0
         return correct / float(eng.y_test_d.numel()), epochs_done
 
     # --------------------------------------------------------------------------------------------
