@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r03full
 rm -rf $O; mkdir -p $O
-timeout -k 10 840 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 840 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 400 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?
 tail -5 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc

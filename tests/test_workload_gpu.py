@@ -145,19 +145,34 @@ def test_config4_tmcs_batched_equals_sequential_reference_loop(cifar20, config4_
     assert np.all(np.isfinite(c.contributivity_scores))
 
 
-def test_config4_coalitions_vs_oracle(cifar20, config4_tmcs):
+def _cifar_oracle_spread(sc, coals, seed):
+    """oracle/cifar_cnn.py v(S) of `coals` (E=1, M=20) run with 3, 8 and the box's CPU threads: [threads][coal]."""
+    import torch
     from oracle import cifar_cnn as occ
-    c = config4_tmcs
-    eng = cifar20.engine
-    ds = cifar20.dataset
+    ds = sc.dataset
     data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    prow = [p.train_idx for p in cifar20.partners_list]
-    bs = [p.batch_size for p in cifar20.partners_list]
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    threads0 = torch.get_num_threads()
+    refs = []
+    for th in sorted({3, 8, threads0}):
+        torch.set_num_threads(th)
+        refs.append([occ.coalition_value(data, prow, bs, k, seed=seed, epochs=1, M=20)[0] for k in coals])
+    torch.set_num_threads(threads0)
+    return np.array(refs)
+
+
+def test_config4_coalitions_vs_oracle(cifar20, config4_tmcs):
+    """Two coalitions of the 20-partner run against oracle/cifar_cnn.py (same keys, schedule, dropout masks).  At
+    E=1 on 2250-row partners these models are barely past chance (accuracy 0.1-0.2), where fp32 summation order
+    alone moves a coalition by points (test_config4_smc_values_are_engine_values_and_vs_oracle): the device
+    must lie inside the oracle's own spread over 3, 8 and the box's CPU threads, widened by 1 pt."""
+    eng = cifar20.engine
     coals = [(5,), (3, 11)]
     dev = np.array([eng.evaluate([k])[0] for k in coals])
-    ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
-    diff = np.abs(dev - ref)
-    assert np.mean(diff) <= 0.01 and np.max(diff) <= 0.03, (dev, ref)
+    refs = _cifar_oracle_spread(cifar20, coals, eng.seed)
+    lo, hi = refs.min(axis=0) - 0.01, refs.max(axis=0) + 0.01
+    assert np.all((lo <= dev) & (dev <= hi)), (coals, dev, refs)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -234,7 +249,6 @@ def test_config4_smc_values_are_engine_values_and_vs_oracle(cifar10p, config4_sm
     thread count: max-pool near-ties route a gradient differently and RMSprop's normalisation spreads it).  So
     the device must land inside the oracle's own spread over thread counts (3, 8 and the box's), widened by
     1 pt."""
-    from oracle import cifar_cnn as occ
     c = config4_smc["SMCS"]
     eng = cifar10p.engine
     keys = [k for k in c.charac_fct_values if len(k) in (1, 2)]
@@ -242,18 +256,7 @@ def test_config4_smc_values_are_engine_values_and_vs_oracle(cifar10p, config4_sm
     picks = [keys[0], keys[-1]] if len(keys) > 1 else keys
     dev = eng.evaluate(picks)
     assert [float(v) for v in dev] == [c.charac_fct_values[k] for k in picks]
-    ds = cifar10p.dataset
-    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    prow = [p.train_idx for p in cifar10p.partners_list]
-    bs = [p.batch_size for p in cifar10p.partners_list]
-    import torch
-    threads0 = torch.get_num_threads()
-    refs = []
-    for th in sorted({3, 8, threads0}):
-        torch.set_num_threads(th)
-        refs.append([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in picks])
-    torch.set_num_threads(threads0)
-    refs = np.array(refs)
+    refs = _cifar_oracle_spread(cifar10p, picks, eng.seed)
     lo, hi = refs.min(axis=0) - 0.01, refs.max(axis=0) + 0.01
     assert np.all((lo <= dev) & (dev <= hi)), (picks, dev, refs)
 
