@@ -707,6 +707,7 @@ def bench_cifar(args, rank, world, sub=False):
     def timed_step(i, planned):
         if s0[0] == 0:
             eng.profiler = None if args.no_kernel_timer else timer
+            eng.time_test_eval = True
             s0[0] = eng.stats["samples"] or -1
         return one_step()
 
@@ -740,6 +741,8 @@ def bench_cifar(args, rank, world, sub=False):
                    "train_samples_per_step_this_rank": int(samples / max(1, steps)),
                    "shapley_estimate": [round(float(v), 5) for v in c.contributivity_scores],
                    "replicas_per_launch": eng.stats.get("replicas", 0) / max(1, eng.stats.get("batches", 1)),
+                   "lockstep_batches": eng.stats.get("batches", 0),
+                   "test_eval_s": round(eng.stats.get("test_eval_s", 0.0), 2),
                    "parallelism": f"coalition-shard x{world}"},
         "budget": {"budget_s": args.budget_s, "steps_requested": args.steps, "warmup_requested": args.warmup,
                    "timed_wall_s": round(wall, 2)},
