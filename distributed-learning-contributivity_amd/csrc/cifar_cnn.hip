@@ -1755,9 +1755,11 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV3_DGRAD_NT 256
 #else  // wave-local form: <HI, WI, CI, CO, PAD, BTY, waves, EPI>
 #define CONV2_FWD wino_wl_kernel<32, 32, 32, 32, 0, 4, 4, EPI_FWD_POOL>      /* 60 tiles, 4 bands, 42 KB */
-#define CONV3_DGRAD wino_wl_kernel<15, 15, 64, 32, 1, 4, 2, EPI_BWD_UNPOOL>  /* 32 tiles, 2 bands, 46.8 KB */
+// conv3's data gradient keeps the row form: its bands hold 2 tile groups, and the wave-local form with 2-wave
+// blocks measured slower (4585 vs 4264 ms over a config #4 run, profiles/r03_driver_bench_v2.json)
+#define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL>        /* 8x8 tiles, 2 bands, 63.7 KB */
 #define CONV2_DGRAD wino_wl_kernel<30, 30, 32, 32, 2, 4, 4, EPI_BWD_MASK>    /* 64 tiles, 4 bands, 44.9 KB */
-#define CONV3_DGRAD_NT 128
+#define CONV3_DGRAD_NT 256
 #endif
 #define CONV3_FWD wino_kernel<15, 15, 32, 64, 1, 8, EPI_FWD>          /* 8x8 tiles,    1 band,  59.7 KB */
 #define CONV4_FWD wino_kernel<15, 15, 64, 64, 0, 6, EPI_FWD_POOL>     /* 6x6 windows,  1 band,  67.9 KB */
