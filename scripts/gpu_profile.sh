@@ -10,7 +10,7 @@ K='conv_bwd_data_kernel|conv_fwd_kernel|conv_wgrad_kernel|dense1_bwd_adam_kernel
 CMD="python bench.py --steps 1 --warmup 1 --no-cpu-baseline"
 # the counter passes run without the bench's in-stream HIP events (a --pmc pass with an event record around
 # every launch crashed rocprofv3's counter thread: SIGSEGV, gpurun_out/profile_r02v6/fetch.err)
-PMC="$CMD --no-kernel-timer"
+PMC="$CMD --no-kernel-timer --no-cifar"
 if [ "$2" != "pmc" ]; then
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $CMD > $O/trace.json 2> $O/trace.err || exit $?
 fi
