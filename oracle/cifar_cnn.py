@@ -179,12 +179,20 @@ def fedavg_round(data, partner_rows, batch_sizes, coalition, glob, seed=0, M=20,
     """One FedAvg round of the CIFAR10 model from the global model `glob` (as oracle/cnn.py fedavg_round): each
     partner a fresh Keras RMSprop over its round rows with the step's keyed dropout masks, then the data-volume
     average.  precise=True: every tensor operation in float64 (same masks, schedule and constants)."""
+    coalition = tuple(sorted(coalition))
+    sizes = [len(partner_rows[p]) for p in coalition]
+    w = np.asarray(sizes) / np.sum(sizes)
+    models = partner_fits(data, partner_rows, batch_sizes, coalition, glob, seed, M, e, m, precise)
+    return ocnn.average_models(glob, models, w, keep_f64=precise)
+
+
+def partner_fits(data, partner_rows, batch_sizes, coalition, glob, seed=0, M=20, e=0, m=0, precise=False):
+    """The partner models of one FedAvg round before the average (fedavg_round), in sorted coalition order
+    (multi_partner_learning.py:301-334: each partner fits a fresh model from the global weights)."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
     mask = sum(1 << p for p in coalition)
     dt = torch.float64 if precise else torch.float32
-    sizes = [len(partner_rows[p]) for p in coalition]
-    w = np.asarray(sizes) / np.sum(sizes)
     models = []
     for p_id in coalition:
         key = ocnn.shuffle_key(seed, mask, p_id)
@@ -195,7 +203,7 @@ def fedavg_round(data, partner_rows, batch_sizes, coalition, glob, seed=0, M=20,
             g, _ = gradients(params, data.x_train[rows], data.y_train[rows], masks, dtype=dt if precise else None)
             opt.step(params, g)
         models.append(params)
-    return ocnn.average_models(glob, models, w, keep_f64=precise)
+    return models
 
 
 def evaluate(p, x, y, batch=500):

@@ -141,6 +141,7 @@ def test_one_step_gradients_and_activations(scenario, engine, odata):
         for k, v in ref_acts.items():
             v = v.reshape(c, -1).numpy()
             assert np.max(np.abs(acts[k][r, :c] - v)) <= 1e-4 * max(1.0, np.max(np.abs(v))), k
+    print(report)
     assert not bad, (bad, report)
 
 
