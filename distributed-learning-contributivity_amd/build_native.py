@@ -37,8 +37,15 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+# Per-source extra flags.  mnist_cnn.hip: no SLP vectorisation - packed f32 VALU (v_pk_add_f32 and the v_mov
+# shuffles that feed it) issued beside f32 MFMAs costs more issue cycles than the scalar ops it replaces
+# (MI355X_MICROARCH.md, per-instruction cycle constants), and it hoisted the Winograd V arithmetic of the
+# software-pipelined conv k-loops out of the MFMA gaps.
+FILE_FLAGS = {"mnist_cnn.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile(src, obj, verbose):
-    cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -226,13 +226,15 @@ __global__ __launch_bounds__(256) void winograd_w2_kernel(const float* __restric
 
 // ------------------------------------------------------------------------------------------------
 // conv1 (recompute) + conv2 (Winograd, MFMA) + bias + ReLU + 2x2 max-pool.  Block = (third of the image:
-// 4 pool rows = 48 tiles, slot, model), 4 waves.  Wave i owns transform row i (xi = 4i .. 4i+3) of the three
-// 16-tile groups x 4 channel groups: 48 accumulators of v_mfma_f32_16x16x4_f32 (tile x co), K = 32 input
-// channels in 8 steps of 4.  A operands (V) are computed in registers from the LDS conv1 tile (8 reads and
-// 8 adds give a lane its 4 values of V for one (tile, ci)); B operands (U, L2-resident) are loaded one
-// k-step ahead.  Output: each wave folds its row of the output transform (T_i = M_i A, 2 values per
-// (tile, co)) into LDS; then Y = sum_i A^T[.][i] T_i + bias, the max over the window (first max in scan
-// order) and ReLU, written with the argmax code.
+// 4 pool rows = 48 tiles, group of FWD_SPB samples, model), 4 waves; the block walks its samples in order.
+// Wave i owns transform row i (xi = 4i .. 4i+3) of the three 16-tile groups x 4 channel groups: 48
+// accumulators of v_mfma_f32_16x16x4_f32 (tile x co), K = 32 input channels in 8 steps of 4.  The wave's B
+// operands (its transform row of U: 128 values) are loaded into registers once per block and serve every
+// group of every sample; A operands (V) are computed in registers from the LDS conv1 tile (8 reads and 8 adds
+// give a lane its 4 values of V for one (tile, ci)), software-pipelined one k-step ahead.  The next sample's
+// image rows are loaded into registers while the current sample's GEMMs run.  Output: each wave folds its row
+// of the output transform (T_i = M_i A, 2 values per (tile, co)) into LDS; then Y = sum_i A^T[.][i] T_i + bias,
+// the max over the window (first max in scan order) and ReLU, written with the argmax code.
 // ------------------------------------------------------------------------------------------------
 constexpr int FWD_THREADS = 256;
 constexpr int FWD_PR = 4;                          // pool rows per block
@@ -243,6 +245,11 @@ constexpr int FWD_C1T = (FWD_C1R * A1 + 31) / 32;  // conv1 tiles (9)
 constexpr int FWD_TILES = FWD_PR * PL;             // 48 Winograd tiles (= pool windows) per block
 constexpr int FWD_TS = C2 + 1;                     // tile stride of a T plane (odd: conflict-free writes)
 constexpr int FWD_TQ = 16 * FWD_TS;                // one (row i, b) plane of T for a 16-tile group
+constexpr int FWD_NIT = (FWD_IMR * IMG + FWD_THREADS - 1) / FWD_THREADS;  // image values per thread
+#ifndef MPLC_FWD_SPB
+#define MPLC_FWD_SPB 9  // samples per block (config #3's bs 27 = 3 groups)
+#endif
+constexpr int FWD_SPB = MPLC_FWD_SPB;
 
 __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -255,53 +262,34 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   __shared__ float img_s[FWD_IMR * IMG];
   __shared__ float a1_s[FWD_C1R * A1 * A1P];
   __shared__ float t_s[8 * FWD_TQ];  // [i][b][16 tiles][64 co]
-  const int64_t lb = xcd_block();  // logical block (part, j, r), replica-major
+  const int64_t lb = xcd_block();  // logical block (part, sample group, r), replica-major
   const int part = (int)(lb % FWD_PARTS);
-  const int j = (int)((lb / FWD_PARTS) % gridDim.y);
+  const int jg = (int)((lb / FWD_PARTS) % gridDim.y);
   const int r = (int)(lb / ((int64_t)FWD_PARTS * gridDim.y));
   const int count = cnt ? cnt[r] : cnt_all;
-  if (j >= count) return;
+  const int j_begin = jg * FWD_SPB;
+  const int j_end = min(count, j_begin + FWD_SPB);
+  if (j_begin >= j_end) return;
   const int tid = threadIdx.x;
-  const int row = idx ? idx[(int64_t)r * bmax + j] : row_base + j;
   const float* P = params + (int64_t)r * stride;
-  const float* xi = x + (int64_t)row * (IMG * IMG) + part * 2 * FWD_PR * IMG;
-  {  // all of the block's image loads in flight at once
-    constexpr int NIT = (FWD_IMR * IMG + FWD_THREADS - 1) / FWD_THREADS;
-    float v[NIT];
+  float imv[FWD_NIT];  // a sample's image rows, loaded one sample ahead
+  auto load_img = [&](int jj) {
+    const int row = idx ? idx[(int64_t)r * bmax + jj] : row_base + jj;
+    const float* xs = x + (int64_t)row * (IMG * IMG) + part * 2 * FWD_PR * IMG;
 #pragma unroll
-    for (int k = 0; k < NIT; ++k) {
+    for (int k = 0; k < FWD_NIT; ++k) {
       const int e = tid + FWD_THREADS * k;
-      v[k] = xi[e < FWD_IMR * IMG ? e : 0];
+      imv[k] = xs[e < FWD_IMR * IMG ? e : 0];
     }
-#pragma unroll
-    for (int k = 0; k < NIT; ++k)
-      if (tid + FWD_THREADS * k < FWD_IMR * IMG) img_s[tid + FWD_THREADS * k] = v[k];
-  }
+  };
+  load_img(j_begin);
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int m = lane & 31;
   const int kh = lane >> 5;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
-  __syncthreads();
-  // conv1 + ReLU for local rows 0..FWD_C1R-1 (global 2*FWD_PR*part + lr): FWD_C1T MFMA tiles over 4 waves
-  constexpr int NPOS1 = FWD_C1R * A1;
-#pragma unroll
-  for (int u = 0; u < (FWD_C1T + 3) / 4; ++u) {
-    const int t = wave + 4 * u;
-    if (t < FWD_C1T) {  // wave-uniform
-      const int p = min(t * 32 + m, NPOS1 - 1);
-      const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int pw = t * 32 + acc_row(reg, kh);
-        if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- Winograd GEMMs: wave = transform row i; lane (tl = lane & 15, kq = lane >> 4)
+  // ---- Winograd GEMM roles: wave = transform row i; lane (tl = lane & 15, kq = lane >> 4)
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
   // B^T row i combines input rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
@@ -309,93 +297,136 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   const int rb = (wi == 3) ? 3 : 2;
   const float sa = (wi == 2) ? -1.0f : 1.0f;
   const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  int pa[3];  // this lane's patch origin (row 2ty + ra, col 2tx) in a1_s for each tile group, + channel kq
-#pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    const int tile = 16 * g + tl;
-    const int ty = tile / PL, tx = tile % PL;
-    pa[g] = ((2 * ty + ra) * A1 + 2 * tx) * A1P + kq;
-  }
   const int drow = (rb - ra) * A1 * A1P;
+  // the wave's B operands of all 8 k-steps (its transform row of U), resident for the whole block
   const float* Ub = U + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C1 * C2 + kq * C2 + tl;
-  auto load_b = [&](int st, float (&bv)[16]) {
+  const float bias = P[OFF_B2 + (tid & 63)];  // the output phase's channel co = tid & 63 in every pass
+  float bw[8][16];
+#pragma unroll
+  for (int st = 0; st < 8; ++st)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-      for (int cg = 0; cg < 4; ++cg) bv[4 * jj + cg] = Ub[(int64_t)jj * C1 * C2 + (4 * st) * C2 + 16 * cg];
-  };
-  float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
-  uint8_t* outc = code ? code + ((int64_t)r * bmax + j) * FEAT : nullptr;
+      for (int cg = 0; cg < 4; ++cg) bw[st][4 * jj + cg] = Ub[(int64_t)jj * C1 * C2 + (4 * st) * C2 + 16 * cg];
 #pragma unroll 1
-  for (int g = 0; g < 3; ++g) {  // one 16-tile group at a time
-    fvec4 acc[4][4];             // [j][channel group]
+  for (int j = j_begin; j < j_end; ++j) {
+    // img_s and a1_s are free: the previous sample's last barrier follows its last reader
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
+    for (int k = 0; k < FWD_NIT; ++k)
+      if (tid + FWD_THREADS * k < FWD_IMR * IMG) img_s[tid + FWD_THREADS * k] = imv[k];
+    if (j + 1 < j_end) load_img(j + 1);  // in flight during this sample's GEMMs
+    __syncthreads();
+    // conv1 + ReLU for local rows 0..FWD_C1R-1 (global 2*FWD_PR*part + lr): FWD_C1T MFMA tiles over 4 waves
+    constexpr int NPOS1 = FWD_C1R * A1;
 #pragma unroll
-      for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-    float bcur[16], bnxt[16];
-    load_b(0, bcur);
+    for (int u = 0; u < (FWD_C1T + 3) / 4; ++u) {
+      const int t = wave + 4 * u;
+      if (t < FWD_C1T) {  // wave-uniform
+        const int p = min(t * 32 + m, NPOS1 - 1);
+        const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
 #pragma unroll
-    for (int st = 0; st < 8; ++st) {
-      if (st + 1 < 8) load_b(st + 1, bnxt);
-      const float* d0 = a1_s + pa[g] + 4 * st;
-      float t[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * A1P] + sb * d0[drow + c * A1P];
-      float v[4];
-      v[0] = t[0] - t[2];
-      v[1] = t[1] + t[2];
-      v[2] = t[2] - t[1];
-      v[3] = t[1] - t[3];
+        for (int reg = 0; reg < 16; ++reg) {
+          const int pw = t * 32 + acc_row(reg, kh);
+          if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
+        }
+      }
+    }
+    __syncthreads();
+    float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
+    uint8_t* outc = code ? code + ((int64_t)r * bmax + j) * FEAT : nullptr;
+#pragma unroll 1
+    for (int g = 0; g < 3; ++g) {  // one 16-tile group at a time
+      const int tile = 16 * g + tl;
+      // this lane's patch origin (row 2ty + ra, col 2tx) in a1_s, + channel kq
+      const int pa = ((2 * (tile / PL) + ra) * A1 + 2 * (tile % PL)) * A1P + kq;
+      fvec4 acc[4][4];  // [j][channel group]
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-        for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = mfma16(v[jj], bcur[4 * jj + cg], acc[jj][cg]);
-      if (st + 1 < 8) {
+        for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+      // Software-pipelined k-loop: the next k-step's 8 patch values are read at the start of a k-step and
+      // pinned (empty asm: the compiler cannot hoist their use) after its first two MFMA chunks, so that their
+      // LDS latency is covered and the next k-step's V arithmetic fills the last two chunks' MFMA gaps.
+      float pn[8];
+      auto load_patch = [&](int st) {
+        const float* d0 = a1_s + pa + 4 * st;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) bcur[q] = bnxt[q];
+        for (int c = 0; c < 4; ++c) {
+          pn[c] = d0[c * A1P];
+          pn[4 + c] = d0[drow + c * A1P];
+        }
+      };
+      auto make_v = [&](float (&v)[4]) {
+        float t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] = sa * pn[c] + sb * pn[4 + c];
+        v[0] = t[0] - t[2];
+        v[1] = t[1] + t[2];
+        v[2] = t[2] - t[1];
+        v[3] = t[1] - t[3];
+      };
+      float vc[4], vn[4];
+      load_patch(0);
+      make_v(vc);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        if (st + 1 < 8) load_patch(st + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          if (jj == 2) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(pn[k]));
+          }
+#pragma unroll
+          for (int cg = 0; cg < 4; ++cg) acc[jj][cg] = mfma16(vc[jj], bw[st][4 * jj + cg], acc[jj][cg]);
+        }
+        if (st + 1 < 8) make_v(vn);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vc[q] = vn[q];
       }
-    }
-    // T_i[b] = sum_j M_ij A[j][b]: T_i0 = M_i0 + M_i1 + M_i2, T_i1 = M_i1 - M_i2 - M_i3.  Lane holds tiles
-    // 4*kq + rr (rr = 0..3) of the group, channel 16*cg + tl.
+      // T_i[b] = sum_j M_ij A[j][b]: T_i0 = M_i0 + M_i1 + M_i2, T_i1 = M_i1 - M_i2 - M_i3.  Lane holds tiles
+      // 4*kq + rr (rr = 0..3) of the group, channel 16*cg + tl.
 #pragma unroll
-    for (int cg = 0; cg < 4; ++cg)
+      for (int cg = 0; cg < 4; ++cg)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float m0 = acc[0][cg][rr], m1 = acc[1][cg][rr], m2 = acc[2][cg][rr], m3 = acc[3][cg][rr];
-        const int o = (4 * kq + rr) * FWD_TS + 16 * cg + tl;
-        t_s[(2 * wi) * FWD_TQ + o] = (m0 + m1) + m2;
-        t_s[(2 * wi + 1) * FWD_TQ + o] = (m1 - m2) - m3;
+        for (int rr = 0; rr < 4; ++rr) {
+          const float m0 = acc[0][cg][rr], m1 = acc[1][cg][rr], m2 = acc[2][cg][rr], m3 = acc[3][cg][rr];
+          const int o = (4 * kq + rr) * FWD_TS + 16 * cg + tl;
+          t_s[(2 * wi) * FWD_TQ + o] = (m0 + m1) + m2;
+          t_s[(2 * wi + 1) * FWD_TQ + o] = (m1 - m2) - m3;
+        }
+      __syncthreads();
+      // Y[a][b] = sum_i A^T[a][i] T_i[b]: Y0b = T0b + T1b + T2b, Y1b = T1b - T2b - T3b; window pixel q = 2a + b
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = tid + FWD_THREADS * k;  // (tile in group, co)
+        const int co = o & 63;
+        const int tile_o = 16 * g + (o >> 6);
+        float tv[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * FWD_TQ + (o >> 6) * FWD_TS + co];
+        float z[4];
+        z[0] = ((tv[0][0] + tv[1][0]) + tv[2][0]) + bias;
+        z[1] = ((tv[0][1] + tv[1][1]) + tv[2][1]) + bias;
+        z[2] = ((tv[1][0] - tv[2][0]) - tv[3][0]) + bias;
+        z[3] = ((tv[1][1] - tv[2][1]) - tv[3][1]) + bias;
+        float best = z[0];
+        int arg = 0;
+#pragma unroll
+        for (int qq = 1; qq < 4; ++qq)
+          if (z[qq] > best) { best = z[qq]; arg = qq; }
+        const int py = FWD_PR * part + tile_o / PL, px = tile_o % PL;
+        const int pidx = (py * PL + px) * C2 + co;
+        outp[pidx] = fmaxf(best, 0.0f);
+        if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
       }
-    __syncthreads();
-    // Y[a][b] = sum_i A^T[a][i] T_i[b]: Y0b = T0b + T1b + T2b, Y1b = T1b - T2b - T3b; window pixel q = 2a + b
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int o = tid + FWD_THREADS * k;  // (tile in group, co)
-      const int co = o & 63;
-      const int tile = 16 * g + (o >> 6);
-      float tv[4][2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) tv[i][bb] = t_s[(2 * i + bb) * FWD_TQ + (o >> 6) * FWD_TS + co];
-      const float bias = P[OFF_B2 + co];
-      float z[4];
-      z[0] = ((tv[0][0] + tv[1][0]) + tv[2][0]) + bias;
-      z[1] = ((tv[0][1] + tv[1][1]) + tv[2][1]) + bias;
-      z[2] = ((tv[1][0] - tv[2][0]) - tv[3][0]) + bias;
-      z[3] = ((tv[1][1] - tv[2][1]) - tv[3][1]) + bias;
-      float best = z[0];
-      int arg = 0;
-#pragma unroll
-      for (int qq = 1; qq < 4; ++qq)
-        if (z[qq] > best) { best = z[qq]; arg = qq; }
-      const int py = FWD_PR * part + tile / PL, px = tile % PL;
-      const int pidx = (py * PL + px) * C2 + co;
-      outp[pidx] = fmaxf(best, 0.0f);
-      if (outc) outc[pidx] = (uint8_t)(arg | (best > 0.0f ? 0x80 : 0));
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -797,7 +828,9 @@ __global__ __launch_bounds__(256) void winograd_w2r_kernel(const float* __restri
 // conv2 data gradient + conv1 backward, Winograd F(2x2, 3x3).  dA1[y][x][ci] = sum_{ky,kx,co} dZ2p[y+ky][x+kx][co]
 // W2r[ky][kx][co][ci] (dZ2p = dZ2 padded by 2) over 13 x 13 output tiles of 2x2 (row-major), as 16 GEMMs
 // M[xi][tile][ci] = sum_co V[xi][tile][co] Ur[xi][co][ci], V = B^T d B of the tile's 4x4 dZ2p patch, K = 64.
-// Block = (band of 64 tiles, sample, replica), 4 waves; wave w owns tiles 16w .. 16w+15 of the band and ALL 16
+// Block = (band of 64 tiles, group of BWD_SPB samples, replica), 4 waves, walking its samples in order (the next
+// sample's first (dp, code) quarter and its image are loaded while the current one finishes); wave w owns
+// tiles 16w .. 16w+15 of the band and ALL 16
 // transform points for both 16-channel halves of ci (32 accumulators of v_mfma_f32_16x16x4_f32).  Per k-step
 // (4 output channels of conv2) a lane reads its tile's 4x4 patch at one channel (16 LDS reads), forms the 16
 // values of V with 32 adds and issues 32 MFMAs with B operands read from the staged Ur quarter (4 x b128 per
@@ -824,6 +857,11 @@ constexpr int BWD_RS = BWD_DC * BWD_CS;        // staged row stride
 constexpr int BWD_PAIRS = BWD_WR * PL * 16;    // (dp, code) pairs of a quarter
 constexpr int BWD_PRE = (BWD_PAIRS + BWD_THREADS - 1) / BWD_THREADS;
 constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quarter [co 16][ci 32][xi 16]
+constexpr int BWD_NIT = (IMG * IMG + BWD_THREADS - 1) / BWD_THREADS;  // image values per thread
+#ifndef MPLC_BWD_SPB
+#define MPLC_BWD_SPB 1  // samples per block (9: +2 % on the probe, the sample loop spills 13 registers)
+#endif
+constexpr int BWD_SPB = MPLC_BWD_SPB;
 static_assert(BWD_BANDS * BWD_BAND_TILES >= BWD_TILES && (BWD_BANDS - 1) * BWD_BAND_TILES < BWD_TILES,
               "MPLC_CNN_W1_BANDS must be ceil(169 / 64)");
 
@@ -835,28 +873,29 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   __shared__ fvec4 ur_s[BWD_UQ / 4];
   __shared__ float img_s[IMG * IMG];
   __shared__ float red_s[4][10 * 32];
-  const int64_t lb = xcd_block();  // logical block (band, j, r), replica-major
+  const int64_t lb = xcd_block();  // logical block (band, sample group, r), replica-major
   const int band = (int)(lb % BWD_BANDS);
-  const int j = (int)((lb / BWD_BANDS) % gridDim.y);
+  const int jg = (int)((lb / BWD_BANDS) % gridDim.y);
   const int r = (int)(lb / ((int64_t)BWD_BANDS * gridDim.y));
-  if (j >= cnt[r]) return;
+  const int j_begin = jg * BWD_SPB;
+  const int j_end = min(cnt[r], j_begin + BWD_SPB);
+  if (j_begin >= j_end) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int tl = lane & 15, kq = lane >> 4;
-  const int row = idx[(int64_t)r * bmax + j];
   const float* P = params + (int64_t)r * stride;
   const int tile0 = band * BWD_BAND_TILES;
   const int ty0 = tile0 / 13;
   const int wy0 = ty0 - 1;  // first window row staged (local window row 0; rows outside 0..11 stay zero)
   const int gt0 = tile0 + 16 * wave;         // this wave's first tile
   const bool active = gt0 < BWD_TILES;       // wave-uniform: the last band's last wave has no tile
-  const float* dp = dPool + ((int64_t)r * bmax + j) * FEAT;
-  const uint8_t* cd = code + ((int64_t)r * bmax + j) * FEAT;
   const fvec4* Uq = reinterpret_cast<const fvec4*>(Ur + (int64_t)r * MPLC_CNN_W2T);
   // pair e of a quarter: channel e & 15, window column (e >> 4) % 12, local window row e / 192
   float pdv[BWD_PRE];
   uint32_t pcd[BWD_PRE];
-  auto fetch = [&](int q) {
+  auto fetch = [&](int jj, int q) {
+    const float* dp = dPool + ((int64_t)r * bmax + jj) * FEAT;
+    const uint8_t* cd = code + ((int64_t)r * bmax + jj) * FEAT;
 #pragma unroll
     for (int s = 0; s < BWD_PRE; ++s) {
       const int e = tid + BWD_THREADS * s;
@@ -867,19 +906,18 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       pcd[s] = ok ? cd[pidx] : 0u;
     }
   };
-  fetch(0);
-  {
-    constexpr int NIT = (IMG * IMG + BWD_THREADS - 1) / BWD_THREADS;
-    const float* xr = x + (int64_t)row * IMG * IMG;
-    float v[NIT];
+  float imv[BWD_NIT];  // a sample's image, loaded ahead of its staging into img_s
+  auto load_img = [&](int jj) {
+    const float* xr = x + (int64_t)idx[(int64_t)r * bmax + jj] * IMG * IMG;
 #pragma unroll
-    for (int k = 0; k < NIT; ++k) {
+    for (int k = 0; k < BWD_NIT; ++k) {
       const int e = tid + BWD_THREADS * k;
-      v[k] = xr[e < IMG * IMG ? e : 0];
+      imv[k] = xr[e < IMG * IMG ? e : 0];
     }
-#pragma unroll
-    for (int k = 0; k < NIT; ++k)
-      if (tid + BWD_THREADS * k < IMG * IMG) img_s[tid + BWD_THREADS * k] = v[k];
+  };
+  fetch(j_begin, 0);
+  load_img(j_begin);
+  {
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
       const int rr = e / (4 * BWD_CS), c = (e / BWD_CS) % 4, k = e % BWD_CS;
@@ -892,6 +930,12 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   // B operand (Ur): ci = 16h + tl, co = 4st + kq of the quarter; chunk m of the 16 transform points at
   // m ^ swz (the staging applies the same XOR)
   const int swz = (tl >> 2) & 3;
+#pragma unroll 1
+  for (int j = j_begin; j < j_end; ++j) {
+  // img_s is free: the previous sample's epilogue reads end before its reduction barrier
+#pragma unroll
+  for (int k = 0; k < BWD_NIT; ++k)
+    if (tid + BWD_THREADS * k < IMG * IMG) img_s[tid + BWD_THREADS * k] = imv[k];
   fvec4 acc[16][2];  // [xi][ci half]
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi)
@@ -935,54 +979,81 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #endif
     }
 #endif
-    if (q < 3) fetch(q + 1);
+    {  // the next quarter's (dp, code), or the next sample's first quarter
+      const int jn = q < 3 ? j : j + 1;
+      if (jn < j_end) fetch(jn, (q + 1) & 3);
+    }
     __syncthreads();
     if (active) {
+      // Software-pipelined k-loop (same operands, same per-accumulator order: bit-identical results).  The
+      // 32 MFMAs of a k-step run as 4 chunks of 8 (transform row i = chunk m: xi = 4m .. 4m+3, both ci
+      // halves); during chunk m the B operands of the next chunk are read, and the next k-step's patch is
+      // read in chunk 0 and turned into its V one transform row per chunk, so that every LDS read has a
+      // chunk of MFMAs (256 cycles) to land and the VALU sits in the MFMA gaps.
+      const float* dq = dz_s + pa;
+      float pn[16];  // next k-step's 4x4 patch, [row][col]
+      auto load_patch = [&](int st) {
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        // B operands first (independent of V): Ur[xi][4st + kq][16h + tl], 4 x b128 per half
-        fvec4 b[2][4];
+        for (int rr2 = 0; rr2 < 4; ++rr2)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const fvec4* ub = ur_s + ((4 * st + kq) * C1 + 16 * h + tl) * 4;
-#pragma unroll
-          for (int m = 0; m < 4; ++m) b[h][m] = ub[m ^ swz];
-        }
-        // V = B^T d B of the 4x4 patch (rows r, columns c) at channel 4st + kq
-        const float* d0 = dz_s + pa + 4 * st;
-        float t[4][4];  // t[i][c] = (B^T d)[i][c]
+          for (int c = 0; c < 4; ++c) pn[4 * rr2 + c] = dq[4 * st + rr2 * BWD_RS + c * BWD_CS];
+      };
+      // transform row i of V from the patch: t_i[c] = (B^T d)[i][c], then v[4i + j] = (t_i B)[j]
+      auto v_row = [&](int i, float (&v)[16]) {
+        float t[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float d_0 = d0[c * BWD_CS], d_1 = d0[BWD_RS + c * BWD_CS];
-          const float d_2 = d0[2 * BWD_RS + c * BWD_CS], d_3 = d0[3 * BWD_RS + c * BWD_CS];
-          t[0][c] = d_0 - d_2;
-          t[1][c] = d_1 + d_2;
-          t[2][c] = d_2 - d_1;
-          t[3][c] = d_1 - d_3;
+          const float d_0 = pn[c], d_1 = pn[4 + c], d_2 = pn[8 + c], d_3 = pn[12 + c];
+          t[c] = (i == 0) ? d_0 - d_2 : (i == 1) ? d_1 + d_2 : (i == 2) ? d_2 - d_1 : d_1 - d_3;
         }
-        float v[16];
+        v[4 * i + 0] = t[0] - t[2];
+        v[4 * i + 1] = t[1] + t[2];
+        v[4 * i + 2] = t[2] - t[1];
+        v[4 * i + 3] = t[1] - t[3];
+      };
+      auto load_b = [&](int st, int m, fvec4 (&b)[2]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[4 * i + 0] = t[i][0] - t[i][2];
-          v[4 * i + 1] = t[i][1] + t[i][2];
-          v[4 * i + 2] = t[i][2] - t[i][1];
-          v[4 * i + 3] = t[i][1] - t[i][3];
+        for (int h = 0; h < 2; ++h) b[h] = ur_s[((4 * st + kq) * C1 + 16 * h + tl) * 4 + (m ^ swz)];
+      };
+      float vc[16], vn[16];
+      load_patch(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v_row(i, vc);
+      fvec4 bc[2], bn[2];
+      load_b(0, 0, bc);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        if (st < 3) load_patch(st + 1);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          if (m < 3) load_b(st, m + 1, bn);
+          else if (st < 3) load_b(st + 1, 0, bn);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            // the patch values "change" here (an empty asm the compiler cannot see through), so the V
+            // arithmetic of row m cannot be hoisted above this chunk and fills its MFMA gaps; in chunk 0
+            // the pin sits after two MFMA pairs, which cover the patch reads issued just before
+            if (x == (m == 0 ? 2 : 0)) {
+              if (m == 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+              for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(pn[k]));
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[4 * m + x][h] = mfma16(vc[4 * m + x], bc[h][x], acc[4 * m + x][h]);
+          }
+          if (st < 3) v_row(m, vn);
+          __builtin_amdgcn_sched_barrier(0);
+          bc[0] = bn[0];
+          bc[1] = bn[1];
         }
-#ifndef BWD_EXP_NOMFMA
 #pragma unroll
-        for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) acc[xi][h] = mfma16(v[xi], b[h][xi >> 2][xi & 3], acc[xi][h]);
-#else  // timing experiment: operands formed and consumed by VALU adds instead of the MFMAs
-#pragma unroll
-        for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) acc[xi][h][0] += v[xi] + b[h][xi >> 2][xi & 3];
-#endif
+        for (int i = 0; i < 16; ++i) vc[i] = vn[i];
       }
     }
   }
   // ---- epilogue (wave-local).  Lane (tl, kq) holds M[xi][tile 4kq + rr][ci 16h + tl] in acc[xi][h][rr].
+  if (j + 1 < j_end) load_img(j + 1);  // in flight during the epilogue
   // conv1 weights as the B operand of the 16x16x4 recompute: W1e[4s + kq][16h + tl], rows 0..8 = taps, 9 = bias
   float w1b[3][2];
 #pragma unroll
@@ -1066,6 +1137,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   float* out = w1_part + (((int64_t)r * bmax + j) * BWD_BANDS + band) * MPLC_CNN_W1P;
   for (int e = tid; e < 10 * 32; e += BWD_THREADS)
     out[e] = (red_s[0][e] + red_s[1][e]) + (red_s[2][e] + red_s[3][e]);
+  }  // samples
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1435,7 +1507,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   // t->w2t holds W2 in Winograd form for the forward, then the rotated kernel's Winograd form for the dgrad
   winograd_w2_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(1);
-  conv_fwd_kernel<<<dim3(FWD_PARTS, B, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->w2t,
+  conv_fwd_kernel<<<dim3(FWD_PARTS, (B + FWD_SPB - 1) / FWD_SPB, R), FWD_THREADS, 0, s>>>(t->x, t->idx, 0, t->cnt, 0, B, t->params, S, t->w2t,
                                                          t->pooled, t->code);
   PROF_END(1);
   }
@@ -1459,7 +1531,7 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   if (ph & MPLC_PHASE_BACK) {
   winograd_w2r_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(5);
-  conv_bwd_data_kernel<<<dim3(BWD_BANDS, B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
+  conv_bwd_data_kernel<<<dim3(BWD_BANDS, (B + BWD_SPB - 1) / BWD_SPB, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
                                                           t->code, t->w1_part);
   PROF_END(5);
   PROF_BEGIN(6);
@@ -1485,7 +1557,7 @@ int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const f
   winograd_w2_kernel<<<dim3(C1 * C2 / 256, n_models), 256, 0, s>>>(params, stride, nullptr, w2_wino);
   for (int s0 = 0; s0 < n_samples; s0 += chunk) {
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
-    conv_fwd_kernel<<<dim3(FWD_PARTS, cn, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
+    conv_fwd_kernel<<<dim3(FWD_PARTS, (cn + FWD_SPB - 1) / FWD_SPB, n_models), FWD_THREADS, 0, s>>>(x, nullptr, s0, nullptr, cn, chunk, params, stride,
                                                                   w2_wino, pooled, nullptr);
     dense_fwd_kernel<<<dim3((cn + 31) / 32, n_models), 256, 0, s>>>(pooled, (int64_t)chunk * FEAT, nullptr, cn, chunk,
                                                                     params, stride, nullptr, nullptr, hidden);

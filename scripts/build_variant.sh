@@ -7,7 +7,7 @@ NAME=$1; shift
 P=distributed-learning-contributivity_amd
 mkdir -p gpurun_ab
 python $P/build_native.py
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I $P/csrc "$@" \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I $P/csrc ${VARIANT_FLAGS--fno-slp-vectorize} "$@" \
   -c ${VARIANT_SRC:-$P/csrc/mnist_cnn.hip} -o /tmp/variant_$NAME.o
 objs=$(ls $P/build/*.o | grep -v "/${VARIANT_BASE:-mnist_cnn}.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o gpurun_ab/$NAME.so $objs /tmp/variant_$NAME.o
