@@ -530,14 +530,58 @@ __device__ __forceinline__ void wino_u_pair(const float* __restrict__ W, float* 
 constexpr int WU_2 = 0, WU_3 = 16 * 32 * 32, WU_4 = WU_3 + 16 * 32 * 64;
 static_assert(WU_4 + 16 * 64 * 64 == MPLC_CIFAR_WT, "MPLC_CIFAR_WT must hold conv2..conv4 in Winograd form");
 
+// The data gradient's kernel (FLIP = 1) reads W transposed, W[k][cout][cin]: one thread per channel pair in
+// U's order would read with a stride of CIN floats, so a block takes a 16 x 16 (cin, cout) tile, reads it
+// cin-fastest, transforms it and writes U cout-fastest through an LDS transpose (same arithmetic per pair).
+template <int CIN, int COUT>
+__device__ __forceinline__ void wino_u_tile_flip(const float* __restrict__ W, float* __restrict__ U, int tile,
+                                                 float (*sx)[16 * 17]) {
+  const int tid = threadIdx.x;
+  const int cin0 = 16 * (tile % (CIN / 16)), cout0 = 16 * (tile / (CIN / 16));
+  const int cin = cin0 + (tid & 15), cout = cout0 + (tid >> 4);  // read order: cin fastest
+  float g[3][3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) g[ky][kx] = W[((2 - ky) * 3 + (2 - kx)) * CIN * COUT + cout * CIN + cin];
+  float gg[4][3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const float col[3] = {g[0][kx], g[1][kx], g[2][kx]};
+    float o[4];
+    wino_g_rows(col, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gg[i][kx] = o[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float o[4];
+    wino_g_rows(gg[i], o);
+#pragma unroll
+    for (int jx = 0; jx < 4; ++jx) sx[4 * i + jx][(tid & 15) * 17 + (tid >> 4)] = o[jx];  // [xi][cin_l][cout_l], row stride 17
+  }
+  __syncthreads();
+  const int wcin = cin0 + (tid >> 4), wcout = cout0 + (tid & 15);  // write order: cout fastest
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) U[xi * CIN * COUT + wcin * COUT + wcout] = sx[xi][(tid >> 4) * 17 + (tid & 15)];
+}
+
 template <int FLIP>
 __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ params, int64_t stride,
                                                      const int32_t* __restrict__ cnt, float* __restrict__ U) {
   const int r = blockIdx.y;
   if (cnt && cnt[r] == 0) return;
-  const int e = blockIdx.x * 256 + threadIdx.x;  // pair index over conv2 (1024) | conv3 (2048) | conv4 (4096)
   const float* P = params + (int64_t)r * stride;
   float* Ur = U + (int64_t)r * MPLC_CIFAR_WT;
+  if (FLIP) {  // 16 x 16 tiles: conv2 4 | conv3 8 | conv4 16 (the grid's 28 blocks per replica)
+    __shared__ float sx[16][16 * 17];
+    const int b = blockIdx.x;
+    if (b < 4) wino_u_tile_flip<32, 32>(P + OFF_W2, Ur + WU_2, b, sx);
+    else if (b < 12) wino_u_tile_flip<64, 32>(P + OFF_W3, Ur + WU_3, b - 4, sx);  // dgrad: in = conv3's 64 co
+    else if (b < 28) wino_u_tile_flip<64, 64>(P + OFF_W4, Ur + WU_4, b - 12, sx);
+    return;
+  }
+  const int e = blockIdx.x * 256 + threadIdx.x;  // pair index over conv2 (1024) | conv3 (2048) | conv4 (4096)
   if (e < 1024) {
     wino_u_pair<32, 32, FLIP>(P + OFF_W2, Ur + WU_2, e);
   } else if (e < 3072) {
