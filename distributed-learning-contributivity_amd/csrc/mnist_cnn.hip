@@ -1261,7 +1261,11 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = wave + 4 * u;
+#ifdef WG_EXP_NOCONV1  // timing experiment switch (garbage results): conv1 recompute compiled out
+        if (false) {
+#else
         if (t < 5) {
+#endif
           const int p = min(t * 32 + m, 6 * A1 - 1);
           const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
 #pragma unroll
@@ -1276,7 +1280,11 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       __syncthreads();
       // 6 k-steps of 4 tiles (window (wr, wc) = tile 12*wr + wc of the band; lane kq takes tile 4*st + kq)
 #pragma unroll 1
+#ifdef WG_EXP_NOGEMM  // timing experiment switch (garbage results): the k-loop compiled out
+      for (int st = 0; st < 0; ++st) {
+#else
       for (int st = 0; st < 6; ++st) {
+#endif
         const int tb = 4 * st + kq;
         const int wr = tb / PL, wc = tb % PL;
         // V: B^T d B of the tile's 4x4 conv1 patch (rows 2*wr .., columns 2*wc ..), channels tl, 16 + tl
