@@ -2,5 +2,5 @@
 # shape; the probe prints the v(S) hash (bit-identical results expected)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-AB_VARIANTS="${AB_VARIANTS:-new wnogemm wnoconv1}" timeout -k 10 900 bash scripts/gpu_ab.sh 252 1 5
-for v in ${AB_VARIANTS:-new wnogemm wnoconv1}; do grep -o "evals/s.*sha1 [0-9a-f]*" gpurun_out/ab_$v/probe.log | sed "s/^/$v /"; done
+AB_VARIANTS="${AB_VARIANTS:-new d1nc new d1nc}" timeout -k 10 900 bash scripts/gpu_ab.sh 252 1 5
+for v in ${AB_VARIANTS:-new d1nc new d1nc}; do grep -o "evals/s.*sha1 [0-9a-f]*" gpurun_out/ab_$v/probe.log | sed "s/^/$v /"; done
