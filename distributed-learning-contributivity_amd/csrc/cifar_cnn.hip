@@ -1063,17 +1063,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   fvec4 acc[16][2];
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi) acc[xi][0] = acc[xi][1] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  auto kstep = [&](int st, const float (&bv)[32]) {
+  // The patch of k-step st + 1 is read right after k-step st's V is formed (its registers are free then), so
+  // that its LDS latency is covered by k-step st's 32 MFMAs instead of stalling ahead of the next k-step's.
+  float pn[16];  // [row][col]
+  auto load_patch = [&](int st) {
     const float* d0 = dpa + 4 * st;
+#pragma unroll
+    for (int rr2 = 0; rr2 < 4; ++rr2)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pn[4 * rr2 + c] = d0[rr2 * ROWP + c * CIP];
+  };
+  load_patch(0);
+  auto kstep = [&](int st, const float (&bv)[32]) {
     float t[4][4];  // t[i][c] = (B^T d)[i][c]
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float d_0 = d0[c * CIP], d_1 = d0[ROWP + c * CIP], d_2 = d0[2 * ROWP + c * CIP], d_3 = d0[3 * ROWP + c * CIP];
+      const float d_0 = pn[c], d_1 = pn[4 + c], d_2 = pn[8 + c], d_3 = pn[12 + c];
       t[0][c] = d_0 - d_2;
       t[1][c] = d_1 + d_2;
       t[2][c] = d_2 - d_1;
       t[3][c] = d_1 - d_3;
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < NK) load_patch(st + 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float v0 = t[i][0] - t[i][2], v1 = t[i][1] + t[i][2], v2 = t[i][2] - t[i][1], v3 = t[i][1] - t[i][3];
