@@ -259,7 +259,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, const float* __restrict__ U,
     float* __restrict__ pooled, uint8_t* __restrict__ code) {
-  __shared__ float img_s[FWD_IMR * IMG];
+  __shared__ float img_s[2][FWD_IMR * IMG];  // double-buffered: the next sample's image goes in beside the current
   __shared__ float a1_s[FWD_C1R * A1 * A1P];
   __shared__ float t_s[8 * FWD_TQ];  // [i][b][16 tiles][64 co]
   const int64_t lb = xcd_block();  // logical block (part, sample group, r), replica-major
@@ -308,14 +308,19 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
       for (int cg = 0; cg < 4; ++cg) bw[st][4 * jj + cg] = Ub[(int64_t)jj * C1 * C2 + (4 * st) * C2 + 16 * cg];
-#pragma unroll 1
-  for (int j = j_begin; j < j_end; ++j) {
-    // img_s and a1_s are free: the previous sample's last barrier follows its last reader
+  auto store_img = [&](float* dst) {
 #pragma unroll
     for (int k = 0; k < FWD_NIT; ++k)
-      if (tid + FWD_THREADS * k < FWD_IMR * IMG) img_s[tid + FWD_THREADS * k] = imv[k];
-    if (j + 1 < j_end) load_img(j + 1);  // in flight during this sample's GEMMs
-    __syncthreads();
+      if (tid + FWD_THREADS * k < FWD_IMR * IMG) dst[tid + FWD_THREADS * k] = imv[k];
+  };
+  store_img(img_s[0]);
+  if (j_begin + 1 < j_end) load_img(j_begin + 1);  // in flight during the first sample
+  __syncthreads();
+#pragma unroll 1
+  for (int j = j_begin; j < j_end; ++j) {
+    // a1_s is free (the previous sample's last two barriers follow its last GEMM read); this sample's image is
+    // in img_s[b] since before the previous sample's barriers
+    const int b = (j - j_begin) & 1;
     // conv1 + ReLU for local rows 0..FWD_C1R-1 (global 2*FWD_PR*part + lr): FWD_C1T MFMA tiles over 4 waves
     constexpr int NPOS1 = FWD_C1R * A1;
 #pragma unroll
@@ -323,13 +328,17 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       const int t = wave + 4 * u;
       if (t < FWD_C1T) {  // wave-uniform
         const int p = min(t * 32 + m, NPOS1 - 1);
-        const floatx16 a = conv1_mfma(img_s, (p / A1) * IMG + p % A1, kh, w1r);
+        const floatx16 a = conv1_mfma(img_s[b], (p / A1) * IMG + p % A1, kh, w1r);
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int pw = t * 32 + acc_row(reg, kh);
           if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
         }
       }
+    }
+    if (j + 1 < j_end) {  // img_s[b ^ 1] was last read by the previous sample's conv1, two barriers ago
+      store_img(img_s[b ^ 1]);
+      if (j + 2 < j_end) load_img(j + 2);
     }
     __syncthreads();
     float* outp = pooled + ((int64_t)r * bmax + j) * FEAT;
