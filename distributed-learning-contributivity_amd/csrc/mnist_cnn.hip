@@ -260,7 +260,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, const float* __restrict__ U,
     float* __restrict__ pooled, uint8_t* __restrict__ code) {
   __shared__ float img_s[2][FWD_IMR * IMG];  // double-buffered: the next sample's image goes in beside the current
-  __shared__ float a1_s[FWD_C1R * A1 * A1P];
+  __shared__ float a1_s[FWD_C1T * 32 * A1P];  // padded to whole conv1 tiles: unconditional writes (rows >= 260 unread)
   __shared__ float t_s[8 * FWD_TQ];  // [i][b][16 tiles][64 co]
   const int64_t lb = xcd_block();  // logical block (part, sample group, r), replica-major
   const int part = (int)(lb % FWD_PARTS);
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int pw = t * 32 + acc_row(reg, kh);
-          if (pw < NPOS1) a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
+          a1_s[pw * A1P + m] = fmaxf(a[reg], 0.0f);
         }
       }
     }
