@@ -1266,24 +1266,36 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         gb += v;
         vq_s[(e >> 6) * WG_VS + (e & 63)] = int2{__float_as_int(v), (int)(c & 3)};
       }
-      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 5 tiles of 32 over the block's waves
+      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 4 tiles of 32 (one per wave, 32x32x2) and the
+      // last 28 positions as 2 x 16 positions x 2 channel halves on 16x16x4 (one piece per wave; a fifth 32x32
+      // tile on wave 0 was 1/8 padding and doubled that wave's share).  Taps and bias in conv1_mfma's k order on
+      // both forms (an exact fmaf chain): bit-identical activations.
+#ifndef WG_EXP_NOCONV1  // timing experiment switch (garbage results): conv1 recompute compiled out
+      {
+        const int p = wave * 32 + m;
+        const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = wave + 4 * u;
-#ifdef WG_EXP_NOCONV1  // timing experiment switch (garbage results): conv1 recompute compiled out
-        if (false) {
-#else
-        if (t < 5) {
-#endif
-          const int p = min(t * 32 + m, 6 * A1 - 1);
-          const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
+        for (int reg = 0; reg < 16; ++reg)
+          a1_s[(wave * 32 + acc_row(reg, kh)) * WG_CS + 2 * (m & 15) + (m >> 4)] = fmaxf(a[reg], 0.0f);
+      }
+      {
+        const int mt = wave >> 1, h = wave & 1, tl = lane & 15, kq = lane >> 4;
+        const int p = min(128 + 16 * mt + tl, 6 * A1 - 1);
+        fvec4 c1 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int reg = 0; reg < 16; ++reg) {
-            const int pw = min(t * 32 + acc_row(reg, kh), 6 * A1 - 1);  // clamped rows rewrite row 155's value
-            a1_s[pw * WG_CS + 2 * (m & 15) + (m >> 4)] = fmaxf(a[reg], 0.0f);
-          }
+        for (int s3 = 0; s3 < 3; ++s3) {
+          const int k = 4 * s3 + kq;
+          const float av = (k < 9) ? img_s[(4 * band + p / A1 + k / 3) * IMG + p % A1 + k % 3] : ((k == 9) ? 1.0f : 0.0f);
+          const float wv = (k < 9) ? P[OFF_W1 + k * C1 + 16 * h + tl] : ((k == 9) ? P[OFF_B1 + 16 * h + tl] : 0.0f);
+          c1 = mfma16(av, wv, c1);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {  // rows past 155 are position 155 again: the same value rewritten
+          const int pw = min(128 + 16 * mt + 4 * kq + reg, 6 * A1 - 1);
+          a1_s[pw * WG_CS + 2 * tl + h] = fmaxf(c1[reg], 0.0f);
         }
       }
+#endif
       if (band < 5) fetch(j, band + 1);
       else if (j + 1 < j_end) fetch(j + 1, 0);
       __syncthreads();
