@@ -7,7 +7,7 @@
 //                   output tile = one pooling window) -> +b, ReLU, 2x2 max-pool -> pooled + argmax code
 //   dense_fwd       Dense(128)+ReLU: per-replica GEMM [b x 9216] x [9216 x 128], fp32 MFMA
 //   head            Dense(10), softmax-CE gradient, dW4/db4 + Adam, dh = dlogits W4^T * relu'
-//   dense1_bwd_adam per 64-row slice of W3: dp = dh W3^T, dW3 = p^T dh, Adam(W3) in the same pass
+//   dense1_bwd_adam per 32-row slice of W3: dp = dh W3^T, dW3 = p^T dh, Adam(W3) in the same pass
 //                   (W3 = 98% of the parameters: read once, written once per step)
 //   winograd_w2r    W2 rotated by 180 degrees, channels swapped, in Winograd form (dgrad B operand)
 //   conv_bwd_data   dA1 = dZ2 (*) W2 in Winograd form F(2x2,3x3) on MFMA, V built directly from (dp, argmax
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense(128) backward + Adam, per 64-row slice of W3 (block = 256 threads: row = tid/4, 32 cols each)
+// Dense(128) backward + Adam, per 32-row slice of W3 (block = 256 threads: row = tid/8, 16 cols each)
 // dp[j][k] = sum_c dh[j][c] W3[k][c];  dW3[k][c] = sum_j p[j][k] dh[j][c];  db3 (slice 0 block)
 // ------------------------------------------------------------------------------------------------
 constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
@@ -1301,7 +1301,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       __syncthreads();
       // 6 k-steps of 4 tiles (window (wr, wc) = tile 12*wr + wc of the band; lane kq takes tile 4*st + kq)
 #pragma unroll 1
-#ifdef WG_EXP_NOGEMM  // timing experiment switch (garbage results): the k-loop compiled out
+#ifdef WG_EXP_NOGEMM  // timing experiment switch (garbage results; the dead staging is compiled out with it)
       for (int st = 0; st < 0; ++st) {
 #else
       for (int st = 0; st < 6; ++st) {
