@@ -672,14 +672,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const uint8_t* cd = (EPI == EPI_BWD_UNPOOL) ? a.code_in + slot * (HO * WO * CO) : nullptr;
   uint8_t* oc = (POOL && a.drop_key) ? a.code_out + slot * (PH * PW * CO) : nullptr;
   const uint32_t rseed = (POOL && a.drop_key) ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
-  // When the wave's whole transform row of U fits 128 registers (conv3 forward and data gradient), it is loaded
-  // once for all the band's groups instead of from L2 per group and k-step (same operands: bit-identical).
-  constexpr bool BREG = 4 * NCG * NK <= 128;
-  float bw[BREG ? NK : 1][4 * NCG];
-  if constexpr (BREG) {
+  // The wave's transform row of U for the first KR k-steps (up to 128 values: all of conv3's, a quarter of conv4's)
+  // is loaded once for all the band's groups instead of from L2 per group and k-step; the rest streams from L2
+  // two k-steps ahead (same operands in the same order: bit-identical).
+  constexpr int BREGS = (4 * NCG * NK <= 128) ? 128 : 64;  // conv4: 64 (128 spilled 41 registers)
+  constexpr int KR = (BREGS / (4 * NCG)) < NK ? BREGS / (4 * NCG) : NK;
+  static_assert(KR % 2 == 0 && (NK - KR) % 2 == 0, "k-steps in pairs");
+  float bw[KR][4 * NCG];
 #pragma unroll
-    for (int st = 0; st < NK; ++st) load_b(st, bw[st]);
-  }
+  for (int st = 0; st < KR; ++st) load_b(st, bw[st]);
   __syncthreads();
 #pragma unroll 1
   for (int g = 0; g < NG; ++g) {
@@ -709,15 +710,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) acc[jj][cg] = mfma16(v[jj], bv[NCG * jj + cg], acc[jj][cg]);
     };
-    static_assert(NK % 2 == 0, "k-steps in pairs");
-    if constexpr (BREG) {
+    float b0[4 * NCG], b1[4 * NCG];
+    if constexpr (KR < NK) load_b(KR, b0);  // in flight during the register k-steps
 #pragma unroll
-      for (int st = 0; st < NK; ++st) kstep(st, bw[st]);
-    } else {
-      float b0[4 * NCG], b1[4 * NCG];
-      load_b(0, b0);
+    for (int st = 0; st < KR; ++st) kstep(st, bw[st]);
+    if constexpr (KR < NK) {
 #pragma unroll 1
-      for (int st = 0; st < NK; st += 2) {
+      for (int st = KR; st < NK; st += 2) {
         load_b(st + 1, b1);
         kstep(st, b0);
         if (st + 2 < NK) load_b(st + 2, b0);
