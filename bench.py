@@ -745,6 +745,14 @@ def bench_cifar(args, rank, world, sub=False):
     achieved = flops / (kern_ms / 1000) / 1e12 if kern_ms > 0 else 0.0
     evals = c.first_charac_fct_calls_count
     coals = [k for k in c.charac_fct_values if len(k)]
+    if getattr(args, "dump_values", None) and rank == 0:
+        # every coalition value this run trained (counted and speculative) as bitmask -> v(S): input of the
+        # planner simulations (scripts/sim_tmcs_planning.py)
+        cache = dict(sc.coalition_values)
+        cache.update({k: v for k, v in c.charac_fct_values.items() if len(k)})
+        masks = np.array([sum(1 << i for i in k) for k in cache], dtype=np.int64)
+        np.savez(args.dump_values, masks=masks, values=np.array(list(cache.values()), dtype=np.float64),
+                 counted=np.array([sum(1 << i for i in k) for k in coals], dtype=np.int64))
     out = {
         "metric": f"coalition v(S) evals/sec (CIFAR10 FedAvg, {args.method})",
         "value": round(evals * steps / wall, 3), "unit": "coalition evals/s", "n_gpus": world,
@@ -821,6 +829,7 @@ def main():
                     help="train leg at the reference's stopping rule (with --epochs 40: its defaults)")
     ap.add_argument("--mnist-signal", type=float, default=0.0,
                     help="class-template signal of the synthetic MNIST (0: random labels)")
+    ap.add_argument("--dump-values", default=None, help="cifar leg: save the trained v(S) values (npz) here")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()

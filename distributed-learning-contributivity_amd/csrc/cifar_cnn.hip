@@ -10,13 +10,13 @@
 //   head           Dense(10) + softmax-CE gradient, dW6 + RMSprop, dh5 = (dl W6^T) * dropout' * relu'
 //   dense5_bwd     per 16-row slice of W5: dd4 = dh5 W5^T, dW5 = d4^T dh5, RMSprop(W5) in one pass; the
 //                  epilogue routes dd4 through dropout' and the pool into the dense dz4 (relu' included)
-//   transpose_w    W2|W3|W4 -> flipped [kyx'][co][ci] for the data-gradient GEMMs
+//   wino_u<1>      W2|W3|W4 -> the rotated, channel-swapped kernels in Winograd form for the data gradients
 //   conv4 wgrad/dgrad, conv3 wgrad/dgrad (epilogue: dropout' + un-pool into dz2), conv2 wgrad/dgrad,
-//   conv1 wgrad    data gradients are the same implicit-GEMM kernel as the forward (full/same padding,
-//                  flipped weights) with a relu'-mask epilogue; weight gradients are split-K over fixed
+//   conv1 wgrad    data gradients are Winograd F(2x2,3x3) like the forward (full/same padding, rotated
+//                  weights) with a relu'-mask epilogue; weight gradients are split-K over fixed
 //                  groups of MPLC_CIFAR_WG_SAMPLES samples (sums independent of the batch composition)
 //   rmsprop_small  RMSprop on W1..b4 from the split partials (fixed order: bitwise reproducible)
-// Everything is fp32 (the reference's Keras float32), accumulated on the exact-f32 MFMA 32x32x2.
+// Everything is fp32 (the reference's Keras float32), accumulated on the exact-f32 MFMAs (32x32x2, 16x16x4).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,8 +40,6 @@ constexpr int HID = MPLC_CIFAR_H5;   // 512
 constexpr int NCLS = 10;
 constexpr int WGS = MPLC_CIFAR_WG_SAMPLES;
 constexpr int WPART = MPLC_CIFAR_WPART;
-// flipped weights for the data gradients, per replica: W2f @0 [9][32][32], W3f @9216 [9][64][32], W4f @27648
-constexpr int WT_W2 = 0, WT_W3 = 9216, WT_W4 = 27648;
 
 // dropout (Keras Dropout -> tf.nn.dropout: (x * (1/(1-rate))) * (u >= rate)); u = 24-bit keyed counter
 constexpr uint32_t DROP_L2 = 2, DROP_L4 = 4, DROP_L5 = 5;
@@ -169,26 +167,6 @@ __global__ void schedule_kernel(const mplc_replica_t* __restrict__ reps, int n_r
     drop_key[r] = ss.dkey;
     // a FedAvg partner's first step of a round starts from the coalition model: W5 from its glob row
     if (w5src) w5src[r] = (reps[r].kind == MPLC_REP_FEDAVG && ss.at == 1) ? rep_glob[r] : -1;
-  }
-}
-
-// wt[kyx'][co][ci] = W[8 - kyx'][ci][co] for W2 (32x32), W3 (32x64), W4 (64x64)
-__global__ void transpose_w_kernel(const float* __restrict__ params, const int32_t* __restrict__ cnt,
-                                   float* __restrict__ wt) {
-  const int r = blockIdx.y;
-  if (cnt[r] == 0) return;
-  const float* P = params + (int64_t)r * STRIDE;
-  float* T = wt + (int64_t)r * MPLC_CIFAR_WT;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < MPLC_CIFAR_WT; e += gridDim.x * blockDim.x) {
-    int ci_n, co_n, base, off;
-    if (e < WT_W3) { ci_n = 32; co_n = 32; base = WT_W2; off = OFF_W2; }
-    else if (e < WT_W4) { ci_n = 32; co_n = 64; base = WT_W3; off = OFF_W3; }
-    else { ci_n = 64; co_n = 64; base = WT_W4; off = OFF_W4; }
-    const int l = e - base;
-    const int kyx = l / (ci_n * co_n);
-    const int rem = l % (ci_n * co_n);
-    const int co = rem / ci_n, ci = rem % ci_n;
-    T[e] = P[off + ((8 - kyx) * ci_n + ci) * co_n + co];
   }
 }
 
@@ -1872,11 +1850,12 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
                      const int32_t* cnt, int cnt_all, const float* params, int64_t stride, const uint64_t* drop_key,
                      float* a1, float* d2, uint8_t* code2, float* a3, float* d4, uint8_t* code4, float* h5,
                      uint8_t* code5, int prof, void* pb, void* pe, float* wu, const float* glob = nullptr,
-                     const int32_t* w5src = nullptr) {
+                     const int32_t* w5src = nullptr, bool make_wu = true) {
 #define PB(k) cifar_prof_record(prof, pb, (k), s)
 #define PE(k) cifar_prof_record(prof, pe, (k), s)
-  // conv2..conv4 weights in Winograd form (U = G g G^T per channel pair)
-  wino_u_kernel<0><<<dim3(7168 / 256, R), 256, 0, s>>>(params, stride, cnt, wu);
+  // conv2..conv4 weights in Winograd form (U = G g G^T per channel pair); the evaluation makes them once for
+  // all its sample chunks (make_wu = false here)
+  if (make_wu) wino_u_kernel<0><<<dim3(7168 / 256, R), 256, 0, s>>>(params, stride, cnt, wu);
   ConvArgs c1 = conv_args(x, in_mode, row_base, idx, cnt, cnt_all, B, params + OFF_W1, stride);
   c1.bias = params + OFF_B1;
   c1.b_rstride = stride;
@@ -1926,6 +1905,27 @@ extern "C" {
 int mplc_cifar_stride(void) { return MPLC_CIFAR_STRIDE; }
 
 int mplc_cifar_wgrad_split_samples(void) { return WGS; }
+
+int64_t mplc_cifar_layout(int what) {
+  switch (what) {
+    case MPLC_CIFAR_Q_STRIDE: return MPLC_CIFAR_STRIDE;
+    case MPLC_CIFAR_Q_NPARAM: return MPLC_CIFAR_NPARAM;
+    case MPLC_CIFAR_Q_A1: return MPLC_CIFAR_A1;
+    case MPLC_CIFAR_Q_D2: return MPLC_CIFAR_D2;
+    case MPLC_CIFAR_Q_A3: return MPLC_CIFAR_A3;
+    case MPLC_CIFAR_Q_D4: return MPLC_CIFAR_D4;
+    case MPLC_CIFAR_Q_H5: return MPLC_CIFAR_H5;
+    case MPLC_CIFAR_Q_DZ4: return MPLC_CIFAR_DZ4;
+    case MPLC_CIFAR_Q_DZ3: return MPLC_CIFAR_DZ3;
+    case MPLC_CIFAR_Q_DZ2: return MPLC_CIFAR_DZ2;
+    case MPLC_CIFAR_Q_DZ1: return MPLC_CIFAR_DZ1;
+    case MPLC_CIFAR_Q_WT: return MPLC_CIFAR_WT;
+    case MPLC_CIFAR_Q_WPART: return MPLC_CIFAR_WPART;
+    case MPLC_CIFAR_Q_WG_SAMPLES: return WGS;
+    case MPLC_CIFAR_Q_TRAIN_T_BYTES: return (int64_t)sizeof(mplc_cifar_train_t);
+    default: return -1;
+  }
+}
 
 int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
   if (!params || !keys || n_models < 1 || n_models > 65535 || stride != MPLC_CIFAR_STRIDE) return MPLC_E_ARG;
@@ -2027,10 +2027,12 @@ int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const
   float* d4 = a3 + mc * MPLC_CIFAR_A3;
   float* h5 = d4 + mc * MPLC_CIFAR_D4;
   float* wu = h5 + mc * MPLC_CIFAR_H5;  // [n_models][MPLC_CIFAR_WT] conv2..conv4 in Winograd form
+  // the weights do not change between chunks: their Winograd form once for the whole evaluation
+  wino_u_kernel<0><<<dim3(7168 / 256, n_models), 256, 0, s>>>(params, stride, nullptr, wu);
   for (int s0 = 0; s0 < n_samples; s0 += chunk) {
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
     enqueue_forward(s, n_models, chunk, x, 2, s0, nullptr, nullptr, cn, params, stride, nullptr, a1, d2, nullptr, a3,
-                    d4, nullptr, h5, nullptr, 0, nullptr, nullptr, wu);
+                    d4, nullptr, h5, nullptr, 0, nullptr, nullptr, wu, nullptr, nullptr, false);
     eval_head_kernel<<<n_models, 256, 0, s>>>(h5, cn, chunk, labels, s0, params, stride, correct, loss_sum);
     const int st = launch_status();
     if (st) return st;

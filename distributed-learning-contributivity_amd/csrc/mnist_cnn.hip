@@ -24,6 +24,13 @@
 #include "mplc_hip.h"
 #include "keyed.h"
 
+// Timing-experiment switches compile parts of a kernel out and give WRONG results by design (A/B probes of
+// where a kernel's time goes).  A product build must never carry one.
+#if (defined(BWD_EXP_NOSTAGE) || defined(BWD_EXP_NOSTAGE_UR) || defined(BWD_EXP_NOSTAGE_DZ) || \
+     defined(BWD_EXP_NOEPI) || defined(WG_EXP_NOCONV1) || defined(WG_EXP_NOGEMM)) && !defined(MPLC_EXPERIMENT)
+#error "a *_EXP_* timing switch produces wrong results: define MPLC_EXPERIMENT for an A/B experiment build"
+#endif
+
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -1488,6 +1495,24 @@ extern "C" {
 int mplc_cnn_stride(void) { return MPLC_CNN_STRIDE; }
 
 int mplc_cnn_wgrad_split_samples(void) { return WG_SAMPLES; }
+
+int64_t mplc_cnn_layout(int what) {
+  switch (what) {
+    case MPLC_CNN_Q_STRIDE: return MPLC_CNN_STRIDE;
+    case MPLC_CNN_Q_NPARAM: return MPLC_CNN_NPARAM;
+    case MPLC_CNN_Q_FEAT: return MPLC_CNN_FEAT;
+    case MPLC_CNN_Q_HID: return MPLC_CNN_HID;
+    case MPLC_CNN_Q_W1P: return MPLC_CNN_W1P;
+    case MPLC_CNN_Q_W2P: return MPLC_CNN_W2P;
+    case MPLC_CNN_Q_W2T: return MPLC_CNN_W2T;
+    case MPLC_CNN_Q_W1_BANDS: return MPLC_CNN_W1_BANDS;
+    case MPLC_CNN_Q_WG_SAMPLES: return WG_SAMPLES;
+    case MPLC_CNN_Q_PROF_KERNELS: return MPLC_PROF_KERNELS;
+    case MPLC_CNN_Q_TRAIN_T_BYTES: return (int64_t)sizeof(mplc_cnn_train_t);
+    case MPLC_CNN_Q_REPLICA_T_BYTES: return (int64_t)sizeof(mplc_replica_t);
+    default: return -1;
+  }
+}
 
 int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream) {
   if (!params || !keys || n_models < 1 || n_models > 65535 || stride < MPLC_CNN_NPARAM) return MPLC_E_ARG;

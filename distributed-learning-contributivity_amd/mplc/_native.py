@@ -36,6 +36,7 @@ SIGNATURES = {
     # batched CNN trainer (include/mplc_hip_cnn.h); mplc.cnn re-binds train_step with its struct type
     "mplc_cnn_stride": (c_int, []),
     "mplc_cnn_wgrad_split_samples": (c_int, []),
+    "mplc_cnn_layout": (c_int64, [c_int]),
     "mplc_cnn_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cnn_copy_rows": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cnn_train_step": (c_int, [c_void_p, c_void_p]),
@@ -46,6 +47,7 @@ SIGNATURES = {
     # batched CIFAR10 CNN trainer (include/mplc_hip_cifar.h); mplc.cifar re-binds train_step with its struct
     "mplc_cifar_stride": (c_int, []),
     "mplc_cifar_wgrad_split_samples": (c_int, []),
+    "mplc_cifar_layout": (c_int64, [c_int]),
     "mplc_cifar_init_params": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "mplc_cifar_train_step": (c_int, [c_void_p, c_void_p]),
     "mplc_cifar_eval_workspace_floats": (c_int64, [c_int, c_int]),
@@ -58,7 +60,14 @@ SIGNATURES = {
                                c_void_p]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/mplc_hip.h MPLC_ABI_VERSION
+
+
+def check_layout(query, expected, what):
+    """Compare the library's layout items (query(i) for i, value in expected) with the host's constants."""
+    bad = {name: (int(query(i)), v) for name, (i, v) in expected.items() if int(query(i)) != int(v)}
+    if bad:
+        raise RuntimeError(f"libmplc_hip.so {what} layout mismatch (library, host): {bad}; rebuild the library")
 
 
 def lib_path():

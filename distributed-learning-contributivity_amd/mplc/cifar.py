@@ -65,11 +65,17 @@ def _bind():
         return
     _native.register("mplc_cifar_train_step", ctypes.c_int, [ctypes.POINTER(CifarTrainT), ctypes.c_void_p])
     lib = _native.lib()
-    if lib.mplc_cifar_stride() != STRIDE:
-        raise RuntimeError("libmplc_hip.so CIFAR layout mismatch; rebuild")
     global WG_SAMPLES
     WG_SAMPLES = int(lib.mplc_cifar_wgrad_split_samples())  # the library's weight-gradient split size
+    _native.check_layout(lib.mplc_cifar_layout, layout_items(), "CIFAR10 CNN")
     _BOUND = True
+
+
+def layout_items():
+    """The host's view of every MPLC_CIFAR_Q_* layout item (include/mplc_hip_cifar.h): name -> (query id, value)."""
+    return {"STRIDE": (0, STRIDE), "NPARAM": (1, NPARAM), "A1": (2, A1), "D2": (3, D2), "A3": (4, A3), "D4": (5, D4),
+            "H5": (6, H5), "DZ4": (7, DZ4), "DZ3": (8, DZ3), "DZ2": (9, DZ2), "DZ1": (10, DZ1), "WT": (11, WT),
+            "WPART": (12, WPART), "WG_SAMPLES": (13, WG_SAMPLES), "TRAIN_T_BYTES": (14, ctypes.sizeof(CifarTrainT))}
 
 
 class CifarModel:
@@ -183,7 +189,10 @@ class CifarModel:
         stream = _native.stream_handle(dev)
         n = int(y.numel())
         C = sel.shape[0]
-        chunk = int(max(16, min(n, eng.eval_budget_bytes // max(1, C * EVAL_FLOATS * 4))))
+        # the workspace also holds every model's Winograd weights (C * WT floats, mplc_cifar_eval_workspace_floats):
+        # the activation chunk gets the rest of the budget
+        budget = max(0, eng.eval_budget_bytes - C * WT * 4)
+        chunk = int(max(16, min(n, budget // max(1, C * EVAL_FLOATS * 4))))
         chunk = min(chunk, 65535)
         ws = torch.empty(int(self.lib.mplc_cifar_eval_workspace_floats(C, chunk)), dtype=torch.float32, device=dev)
         correct = torch.zeros(C, dtype=torch.int32, device=dev)

@@ -98,11 +98,18 @@ def _bind():
     _native.register("mplc_cnn_train_step", c_int, [ctypes.POINTER(TrainT), vp])
     _native.register("mplc_cnn_evaluate", c_int, [vp, c_int64, c_int, vp, vp, c_int, c_int, vp, vp, vp, vp, vp, vp])
     lib = _native.lib()
-    if lib.mplc_cnn_stride() != STRIDE:
-        raise RuntimeError("libmplc_hip.so CNN layout mismatch; rebuild")
     global WG_SAMPLES
     WG_SAMPLES = int(lib.mplc_cnn_wgrad_split_samples())  # the library's conv2 weight-gradient split size
+    _native.check_layout(lib.mplc_cnn_layout, layout_items(), "MNIST CNN")
     _BOUND = True
+
+
+def layout_items():
+    """The host's view of every MPLC_CNN_Q_* layout item (include/mplc_hip_cnn.h): name -> (query id, value)."""
+    return {"STRIDE": (0, STRIDE), "NPARAM": (1, NPARAM), "FEAT": (2, FEAT), "HID": (3, HID), "W1P": (4, W1P),
+            "W2P": (5, W2P), "W2T": (6, W2T), "W1_BANDS": (7, W1_BANDS), "WG_SAMPLES": (8, WG_SAMPLES),
+            "PROF_KERNELS": (9, len(KERNEL_IDS)), "TRAIN_T_BYTES": (10, ctypes.sizeof(TrainT)),
+            "REPLICA_T_BYTES": (11, ctypes.sizeof(ReplicaT))}
 
 
 # ------------------------------------------------------------------------------------------------

@@ -229,7 +229,8 @@ class Contributivity:
         coalitions = [list(c) for r in range(1, n + 1) for c in combinations(range(n), r)]
         self.prefetch(coalitions)
         char_values = [self.not_twice_characteristic(c) for c in coalitions]
-        sv = shapley_value(n, char_values)
+        # every rank holds the same (all-reduced) values here, so the sum may be range-sharded across them
+        sv = shapley_value(n, char_values, sharded=True)
         self.name = "Shapley"
         self.contributivity_scores = np.array(sv)
         self.scores_std = np.zeros(len(sv))

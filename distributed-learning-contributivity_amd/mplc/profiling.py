@@ -43,8 +43,9 @@ class KernelTimer:
         keep = []
         for name, a, b in self.pending:
             if block or b.query():
-                self.ms[name] += a.elapsed_time(b)
-                self.count[name] += 1
+                if name in self.ms:
+                    self.ms[name] += a.elapsed_time(b)
+                    self.count[name] += 1
             else:
                 keep.append((name, a, b))
         self.pending = keep
@@ -60,18 +61,24 @@ class KernelTimer:
             a, b = self._event_pair()
             self.pending.append((self.kernel, a, b))
             return a.cuda_event, b.cuda_event
-        n = max(self.ids.values()) + 1
+        # the library records ev[k] for EVERY kernel id of the step (mplc_cnn_train_step / mplc_cifar_train_step),
+        # so the arrays cover all of the model's ids with live events; ids outside `names` are recorded, not counted
+        n = max(self.all_ids.values()) + 1
         begin = (ctypes.c_void_p * n)()
         end = (ctypes.c_void_p * n)()
-        for name, k in self.ids.items():
+        for name, k in self.all_ids.items():
             a, b = self._event_pair()
             begin[k], end[k] = a.cuda_event, b.cuda_event
             self.pending.append((name, a, b))
+        assert all(begin[k] and end[k] for k in range(1, n)), "every kernel id of the step needs an event pair"
         self._keep.append((begin, end))
         return ctypes.addressof(begin), ctypes.addressof(end)
 
     def bind(self, kernel_ids):
-        """Kernel ids of the model being timed (its KERNEL_IDS)."""
+        """Kernel ids of the model being timed (its KERNEL_IDS: ids 1..K, every launch of the step)."""
+        if sorted(kernel_ids.values()) != list(range(1, len(kernel_ids) + 1)):
+            raise ValueError("KERNEL_IDS must number the step's launches 1..K")
+        self.all_ids = dict(kernel_ids)
         self.ids = {n: kernel_ids[n] for n in self.names}
         return self
 

@@ -99,29 +99,34 @@ def sharded_shapley(V, n, rank, world_size):
     return agg.finalize(part).cpu().numpy()
 
 
-def shapley_from_table(V, n):
-    """SV (numpy float64, length n) of a bitmask-ordered table given as numpy array or device tensor.  Under
-    torch.distributed with n >= 16 the table is reduced range-sharded across the ranks (sharded_shapley)."""
+def shapley_from_table(V, n, sharded=False):
+    """SV (numpy float64, length n) of a bitmask-ordered table given as numpy array or device tensor.
+
+    sharded=True is a COLLECTIVE: under torch.distributed with n >= 16 every rank must call it with the same
+    table, which is then reduced range-sharded across the ranks (sharded_shapley).  The default is local, as
+    the reference's pure function (a caller on one rank, e.g. post-processing on rank 0, must not block)."""
     from .parallel import world
     torch = _torch()
     if isinstance(V, np.ndarray):
         V = torch.from_numpy(np.ascontiguousarray(V, dtype=np.float64)).cuda()
     rank, ws = world()
-    if ws > 1 and n >= 16:
+    if sharded and ws > 1 and n >= 16:
         return sharded_shapley(V, n, rank, ws)
     agg = ShapleyAggregator(n, device=V.device)
     return agg.run(V).cpu().numpy()
 
 
-def shapley_value(partners_count, char_func_list):
+def shapley_value(partners_count, char_func_list, sharded=False):
     """Drop-in for the reference ``shapley_value`` (mplc/contributivity.py:1210-1253).
 
     char_func_list: v(S) of the 2^n - 1 non-empty coalitions in combination order (as built by
     compute_SV, mplc/contributivity.py:149-158).  Returns a list of n floats.
     The reference calls quit() for n == 0 (mplc/contributivity.py:1214-1216); this raises ValueError.
+    sharded=True (compute_SV, where every rank holds the all-reduced table): a collective, see
+    shapley_from_table; the default computes locally like the reference's pure function.
     """
     n = int(partners_count)
     if n == 0:
         raise ValueError("No players")
     table = combination_list_to_bitmask(n, char_func_list)
-    return [float(x) for x in shapley_from_table(table, n)]
+    return [float(x) for x in shapley_from_table(table, n, sharded=sharded)]

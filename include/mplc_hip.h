@@ -31,8 +31,9 @@ extern "C" {
 #define MPLC_E_WORKSPACE (-2)  /* workspace too small                                            */
 #define MPLC_E_SHAPE (-3)      /* tensor geometry the kernel does not support                    */
 
-/* Version / capability probe: returns MPLC_ABI_VERSION. */
-#define MPLC_ABI_VERSION 1
+/* Version / capability probe: returns MPLC_ABI_VERSION.  Version 2: the CIFAR10 Winograd weight workspace
+ * (MPLC_CIFAR_WT 114688) and the layout queries mplc_cnn_layout / mplc_cifar_layout. */
+#define MPLC_ABI_VERSION 2
 int mplc_abi_version(void);
 
 /* ------------------------------------------------------------------------------------------------

@@ -133,6 +133,26 @@ int mplc_cifar_stride(void);
 /* Samples per weight-gradient split: mplc_cifar_train_t.wg_splits must be ceil(bmax / this). */
 int mplc_cifar_wgrad_split_samples(void);
 
+/* Layout query (ABI check at load): the value of item `what` (MPLC_CIFAR_Q_*) as this library was built, or -1
+ * for an unknown item.  The host compares every item with its own constants and refuses a mismatched pair. */
+#define MPLC_CIFAR_Q_STRIDE 0
+#define MPLC_CIFAR_Q_NPARAM 1
+#define MPLC_CIFAR_Q_A1 2
+#define MPLC_CIFAR_Q_D2 3
+#define MPLC_CIFAR_Q_A3 4
+#define MPLC_CIFAR_Q_D4 5
+#define MPLC_CIFAR_Q_H5 6
+#define MPLC_CIFAR_Q_DZ4 7
+#define MPLC_CIFAR_Q_DZ3 8
+#define MPLC_CIFAR_Q_DZ2 9
+#define MPLC_CIFAR_Q_DZ1 10
+#define MPLC_CIFAR_Q_WT 11
+#define MPLC_CIFAR_Q_WPART 12
+#define MPLC_CIFAR_Q_WG_SAMPLES 13
+#define MPLC_CIFAR_Q_TRAIN_T_BYTES 14  /* sizeof(mplc_cifar_train_t) */
+#define MPLC_CIFAR_Q_COUNT 15
+int64_t mplc_cifar_layout(int what);
+
 /* glorot_uniform kernels / zero biases for n_models rows, keyed per model. */
 int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream);
 

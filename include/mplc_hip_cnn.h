@@ -82,7 +82,8 @@ typedef struct {
   /* geometry */
   int32_t n_rep;          /* replicas                                                     */
   int32_t bmax;           /* max batch size over replicas (slot stride)                   */
-  int32_t w2_splits;      /* = ceil(bmax / 8): wgrad splits of 8 samples per replica      */
+  int32_t w2_splits;      /* = ceil(bmax / mplc_cnn_wgrad_split_samples()): conv2 weight- */
+                          /* gradient splits of that many samples per replica (9)           */
   int32_t pad0;
   /* schedule (global step -> per-replica samples) */
   int32_t step;           /* global step index                                            */
@@ -148,6 +149,23 @@ int mplc_cnn_stride(void);
 
 /* Samples per conv2 weight-gradient split: mplc_cnn_train_t.w2_splits must be ceil(bmax / this). */
 int mplc_cnn_wgrad_split_samples(void);
+
+/* Layout query (ABI check at load): the value of item `what` (MPLC_CNN_Q_*) as this library was built, or -1
+ * for an unknown item.  The host compares every item with its own constants and refuses a mismatched pair. */
+#define MPLC_CNN_Q_STRIDE 0
+#define MPLC_CNN_Q_NPARAM 1
+#define MPLC_CNN_Q_FEAT 2
+#define MPLC_CNN_Q_HID 3
+#define MPLC_CNN_Q_W1P 4
+#define MPLC_CNN_Q_W2P 5
+#define MPLC_CNN_Q_W2T 6
+#define MPLC_CNN_Q_W1_BANDS 7
+#define MPLC_CNN_Q_WG_SAMPLES 8
+#define MPLC_CNN_Q_PROF_KERNELS 9
+#define MPLC_CNN_Q_TRAIN_T_BYTES 10    /* sizeof(mplc_cnn_train_t) */
+#define MPLC_CNN_Q_REPLICA_T_BYTES 11  /* sizeof(mplc_replica_t)   */
+#define MPLC_CNN_Q_COUNT 12
+int64_t mplc_cnn_layout(int what);
 
 /* glorot_uniform kernels / zero biases for n_models rows, keyed per model (deterministic counter RNG). */
 int mplc_cnn_init_params(float* params, int64_t stride, const uint64_t* keys, int n_models, void* stream);

@@ -71,8 +71,10 @@ def _worker(rank, world, port, out_q):
     _, table = _table(n)
     c = _compute_sv(n, table)
     V = osh.synthetic_table(20)
-    sv20 = shapley_from_table(V, 20)
-    out_q.put((rank, c.contributivity_scores.tolist(), c.first_charac_fct_calls_count, sv20.tolist()))
+    sv20 = shapley_from_table(V, 20, sharded=True)
+    sv20_local = shapley_from_table(V, 20)  # default: local, no collective
+    out_q.put((rank, c.contributivity_scores.tolist(), c.first_charac_fct_calls_count, sv20.tolist(),
+               sv20_local.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -99,3 +101,4 @@ def test_two_rank_compute_sv_range_sharded():
     assert res[0][2] == single.first_charac_fct_calls_count == 2 ** n - 1
     ref20 = osh.shapley_bitmask_ld(20, osh.synthetic_table(20))
     assert np.max(np.abs(np.array(res[0][3]) - ref20)) <= 1e-12 * np.max(np.abs(ref20))
+    assert np.max(np.abs(np.array(res[0][4]) - ref20)) <= 1e-12 * np.max(np.abs(ref20))
