@@ -263,17 +263,42 @@ class Contributivity:
         table.update(known)
         return table
 
+    def _frontier_plan(self, n, v_all, truncation):
+        """plan(perms, stop) -> keys for one frontier step of a permutation wave (mplc.mc.plan_frontier): the
+        required first unknown prefixes plus speculative deeper prefixes up to `mc_plan_replicas` (default 1024)
+        replicas per rank, so that the lockstep batches stay large when few walks remain (config #4's
+        TMCS batches averaged 92 replicas).  mc_plan_replicas = 0 turns the speculation off."""
+        from .mc import plan_frontier, size_predictor
+        target = int(getattr(self.scenario, "mc_plan_replicas", 1024)) * self._world_size()
+        cache = self._cache()
+        known = self.charac_fct_values
+
+        def value(key):
+            return known[key] if key in known else cache.get(key)
+
+        def plan(perms, stop):
+            pred = size_predictor(((k, v) for d in (cache, known) for k, v in d.items()), n, v_all)
+            keys, required = plan_frontier(perms, stop, value, pred, v_all, truncation, target)
+            st = self.__dict__.setdefault("plan_stats", {"frontier_steps": 0, "required": 0, "speculative": 0})
+            st["frontier_steps"] += 1
+            st["required"] += required
+            st["speculative"] += len(keys) - required
+            return keys
+        return plan, value
+
     def _prefetch_permutation_wave(self, n, v_all, truncation, wave, interpolate=False, sizes=None):
         """Draw the next `wave` permutations WITHOUT consuming the global RNG, walk each one's prefixes up
-        to its truncation point level by level, and batch-evaluate every uncached prefix of a level at
-        once.  These are exactly the coalitions the sequential loop will ask for on those permutations.
-        With the MI355X engine the walks and their truncation tests run on device (mplc.mc.wave_frontier,
-        csrc/mc_shapley.hip); a plain evaluator (CPU test harness) is walked here in Python."""
+        to its truncation point, and batch-evaluate the uncached prefixes the walks stop on (plus speculative
+        deeper ones, _frontier_plan) at once; repeat until every walk is complete.  These are the coalitions
+        the sequential loop will ask for on those permutations.  With the MI355X engine the walks and their
+        truncation tests run on device (mplc.mc.wave_frontier, csrc/mc_shapley.hip); a plain evaluator (CPU test
+        harness) is walked here in Python."""
         if self._batched_evaluator() is None:
             return
         state = np.random.get_state()
-        perms = [np.random.permutation(n) for _ in range(wave)]
+        perms = np.array([np.random.permutation(n) for _ in range(wave)])
         np.random.set_state(state)
+        plan, value = self._frontier_plan(n, v_all, truncation)
         approach = getattr(self.scenario, "multi_partner_learning_approach", None)
         if getattr(approach, "device_planning", False) and n <= 24:
             from .mc import wave_frontier
@@ -281,40 +306,24 @@ class Contributivity:
             def evaluate(keys):
                 self.prefetch(keys)
                 cache = self._cache()
-                return [cache[k] for k in keys]
-            wave_frontier(self._device_table(), np.array(perms), v_all, truncation, interpolate, sizes, evaluate)
+                return [cache[k] if k in cache else self.charac_fct_values[k] for k in keys]
+            wave_frontier(self._device_table(), perms, v_all, truncation, interpolate, sizes, evaluate, plan=plan)
             return
-        cache = self._cache()
-        known = self.charac_fct_values
-
-        def value(key):
-            return known[key] if key in known else cache.get(key)
-
-        char_now = [0.0] * wave
-        pos = [0] * wave
-        active = list(range(wave))
-        while active:
-            need = []
-            still = []
-            for w in active:
-                perm = perms[w]
-                while pos[w] < n:
-                    if abs(v_all - char_now[w]) < truncation:
-                        pos[w] = n  # truncated: no further coalition on this permutation
-                        break
-                    key = tuple(sorted(int(i) for i in perm[:pos[w] + 1]))
-                    v = value(key)
+        while True:
+            stop = np.full(wave, n)
+            for w in range(wave):
+                char = 0.0
+                for j in range(n):
+                    if abs(v_all - char) < truncation:
+                        break  # truncated: no further coalition on this permutation
+                    v = value(tuple(sorted(int(i) for i in perms[w, :j + 1])))
                     if v is None:
-                        need.append(key)
+                        stop[w] = j
                         break
-                    char_now[w] = v
-                    pos[w] += 1
-                if pos[w] < n:
-                    still.append(w)
-            if not need:
-                break
-            self.prefetch(need)
-            active = still
+                    char = v
+            if np.all(stop >= n):
+                return
+            self.prefetch(plan(perms, stop))
 
     def _truncated_loop(self, n, v_all, sv_accuracy, alpha, truncation, interpolate):
         rows = np.zeros((128, n))
@@ -329,6 +338,12 @@ class Contributivity:
                 # GPU's (mc_wave_scale overrides); more permutations per wave only adds speculation
                 scale = int(getattr(self.scenario, "mc_wave_scale", 0) or self._world_size())
                 span = (100 if t < 100 else 50) * scale
+                if t >= 100 and getattr(self.scenario, "mc_wave_adaptive", True):
+                    # past the first 100 walks the stopping rule itself estimates how many walks are still to
+                    # come; drawing half of them at once (at most 8 waves) merges the small tails of consecutive
+                    # waves into one frontier.  Walks the loop then does not make are speculation only.
+                    remaining = q ** 2 * v_max / sv_accuracy ** 2 - t
+                    span = max(span, min(int(0.5 * remaining), 8 * span))
                 self._prefetch_permutation_wave(n, v_all, truncation, span, interpolate, sizes)
                 wave = t + span
             t += 1

@@ -94,15 +94,81 @@ def mask_to_key(mask):
     return tuple(i for i in range(mask.bit_length()) if (mask >> i) & 1)
 
 
-def wave_frontier(table, perms, v_all, truncation, interpolate, sizes, evaluate):
+def size_predictor(known, n, v_all):
+    """v(S) predicted from |S| alone (the speculative planner's truncation guess): per size the mean of the
+    known values of that size, linear in between, v_all at n.  known: iterable of (sorted key, value)."""
+    sums = np.zeros(n + 1)
+    cnt = np.zeros(n + 1)
+    for k, v in known:
+        if 0 < len(k) < n:
+            sums[len(k)] += v
+            cnt[len(k)] += 1
+    sums[n], cnt[n] = v_all, 1
+    xs = [s for s in range(1, n + 1) if cnt[s] > 0]
+    return np.interp(np.arange(n + 1), xs, [sums[s] / cnt[s] for s in xs])
+
+
+def plan_frontier(perms, stop, value, pred, v_all, truncation, target_replicas, margin=0.5):
+    """The coalitions to train for one frontier step of a wave of truncated permutation walks
+    (mplc/contributivity.py:215-246: a walk needs v(perm[:j+1]) while |v_all - v(perm[:j])| >= truncation).
+
+    perms [K][n]; stop[k] = position j of walk k's first unknown prefix perm[:j+1] (n: the walk is complete).
+    Every first unknown prefix is REQUIRED.  While the batch holds fewer than `target_replicas` replicas (one per
+    member), deeper prefixes of the same walks are added level by level as SPECULATION: the walk reaches
+    perm[:j+2] unless its truncation test fires on perm[:j+1] - decided exactly when that value is known, else
+    guessed from pred[|S|] (size_predictor) with the band widened by `margin`.  Speculation never changes a
+    result (v(S) is a function of (S, seed) only, and the sequential loop still decides what it asks for): a
+    wrong guess costs the training of a coalition the loop will not use.
+    value(key) -> known v or None.  Returns (keys, number of required keys); keys are sorted tuples."""
+    perms = np.asarray(perms)
+    K, n = perms.shape
+    chosen = {}
+    replicas = 0
+    chains = []
+    for k in range(K):
+        j = int(stop[k])
+        if j >= n:
+            continue
+        key = tuple(sorted(int(i) for i in perms[k, :j + 1]))
+        if key not in chosen:
+            chosen[key] = True
+            replicas += len(key)
+        chains.append((k, j))
+    required = len(chosen)
+    while chains and replicas < target_replicas:
+        deeper = []
+        for k, j in chains:
+            if j + 1 >= n:
+                continue
+            prev = tuple(sorted(int(i) for i in perms[k, :j + 1]))
+            v = value(prev)
+            if v is not None:
+                if abs(v_all - v) < truncation:
+                    continue  # the walk truncates after prev: nothing deeper is ever asked for
+            elif abs(v_all - pred[j + 1]) < truncation * (1.0 + margin):
+                continue  # likely to truncate there: do not speculate past it
+            key = tuple(sorted(int(i) for i in perms[k, :j + 2]))
+            if key not in chosen and value(key) is None:
+                chosen[key] = True
+                replicas += len(key)
+            deeper.append((k, j + 1))
+        chains = deeper
+    return list(chosen), required
+
+
+def wave_frontier(table, perms, v_all, truncation, interpolate, sizes, evaluate, plan=None):
     """Walk `perms` on device; while walks stop on unknown prefixes, evaluate those prefixes in one batch
-    (`evaluate(list of keys) -> values`), publish them to the table and walk again.  Returns the rows."""
+    (`evaluate(list of keys) -> values`), publish them to the table and walk again.  With `plan`
+    (plan(perms, stop) -> keys, e.g. plan_frontier) the batch also holds speculative deeper prefixes.
+    Returns the rows."""
     while True:
         rows, status, need = tmc_walk(table, perms, v_all, truncation, interpolate, sizes)
-        missing = sorted({int(m) for m, s in zip(need, status) if s < table.n})
-        if not missing:
+        if np.all(status >= table.n):
             return rows
-        keys = [mask_to_key(m) for m in missing]
+        if plan is not None:
+            keys = plan(perms, status)
+        else:
+            keys = [mask_to_key(m) for m in sorted({int(m) for m, s in zip(need, status) if s < table.n})]
         vals = evaluate(keys)
         table.update(dict(zip(keys, (float(v) for v in vals))))
 
@@ -161,4 +227,5 @@ def tmc_moments(table, n_perms, v_all=None, truncation=0.05, interpolate=False, 
     return mean, np.sqrt(var), int(k)
 
 
-__all__ = ["VTable", "tmc_walk", "wave_frontier", "truncated_mc_table", "tmc_moments", "mask_to_key"]
+__all__ = ["VTable", "tmc_walk", "wave_frontier", "truncated_mc_table", "tmc_moments", "mask_to_key", "plan_frontier",
+           "size_predictor"]
