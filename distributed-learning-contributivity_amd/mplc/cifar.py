@@ -114,7 +114,8 @@ class CifarModel:
         u8 = dict(dtype=torch.uint8, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         splits = (B + WG_SAMPLES - 1) // WG_SAMPLES
-        st.rms = torch.zeros((R, STRIDE), **f32)
+        opt = getattr(st, "resume_opt", None)  # a compacted batch continues its replicas' accumulators
+        st.rms = opt["rms"] if opt else torch.zeros((R, STRIDE), **f32)
         st.ws = dict(
             idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), opt_t=torch.empty(R, **i32),
             drop_key=torch.empty(R, dtype=torch.int64, device=dev),
@@ -141,6 +142,11 @@ class CifarModel:
 
     def free(self, st):
         st.rms = None
+
+    @staticmethod
+    def opt_state(st):
+        """The per-replica optimizer rows of a TrainBatch (RMSprop accumulators)."""
+        return {"rms": st.rms}
 
     def step(self, st, s, prof):
         st.t.step = s

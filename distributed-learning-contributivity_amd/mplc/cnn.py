@@ -209,8 +209,9 @@ class MnistModel:
         eng, dev, R, B = st.eng, st.dev, st.R, st.bmax
         f32 = dict(dtype=torch.float32, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
-        st.adam_m = torch.zeros((R, STRIDE), **f32)
-        st.adam_v = torch.zeros((R, STRIDE), **f32)
+        opt = getattr(st, "resume_opt", None)  # a compacted batch continues its replicas' moments
+        st.adam_m = opt["adam_m"] if opt else torch.zeros((R, STRIDE), **f32)
+        st.adam_v = opt["adam_v"] if opt else torch.zeros((R, STRIDE), **f32)
         splits = (B + WG_SAMPLES - 1) // WG_SAMPLES
         st.ws = dict(
             idx=torch.empty((R, B), **i32), cnt=torch.empty(R, **i32), adam_t=torch.empty(R, **i32),
@@ -235,6 +236,11 @@ class MnistModel:
 
     def free(self, st):
         st.adam_m = st.adam_v = None
+
+    @staticmethod
+    def opt_state(st):
+        """The per-replica optimizer rows of a TrainBatch (Adam moments)."""
+        return {"adam_m": st.adam_m, "adam_v": st.adam_v}
 
     def step(self, st, s, prof):
         st.t.step = s
@@ -312,7 +318,11 @@ class TrainBatch:
     """Device state of one lockstep batch: coalition global rows, replica rows, optimizer state, workspaces
     (model-specific parts through eng.model_impl)."""
 
-    def __init__(self, eng, coalitions, epochs, lib, record=False):
+    def __init__(self, eng, coalitions, epochs, lib, record=False, resume=None):
+        """resume (CnnBatchTrainer._compact): continue coalitions of an earlier batch - their coalition rows
+        ("glob"), replica rows ("params") and optimizer rows ("opt", the model's opt_state names) in this batch's
+        order, and that batch's schedule geometry ("round_len", "fed_steps", "total_steps": the step -> (epoch,
+        round, position) map must not change, mplc_hip_cnn.h schedule)."""
         import torch
         self.eng, self.lib = eng, lib
         self.record = record
@@ -375,19 +385,26 @@ class TrainBatch:
         self.round_len = round_len
         self.fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
         self.total_steps = max(self.fed_steps, single_steps)
+        if resume is not None:
+            self.round_len, self.fed_steps, self.total_steps = (resume["round_len"], resume["fed_steps"],
+                                                                resume["total_steps"])
         S = self.model.STRIDE
         f32 = dict(dtype=torch.float32, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.f32, self.i32 = f32, i32
-        self.glob = torch.empty((C, S), **f32)
-        self.params = torch.empty((R, S), **f32)
-        keys = torch.from_numpy(np.array([init_key(eng.seed, sum(1 << p for p in c)) for c in coalitions],
-                                         dtype=np.uint64).view(np.int64)).to(dev)
-        self.model.init_params(self.glob, keys, self.stream)
         src_map = torch.tensor(src, **i32)
         self.src_map = src_map  # replica -> coalition row of glob
-        _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), S,
-                                             _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
+        if resume is not None:
+            self.glob, self.params = resume["glob"], resume["params"]
+            assert tuple(self.glob.shape) == (C, S) and tuple(self.params.shape) == (R, S)
+        else:
+            self.glob = torch.empty((C, S), **f32)
+            self.params = torch.empty((R, S), **f32)
+            keys = torch.from_numpy(np.array([init_key(eng.seed, sum(1 << p for p in c)) for c in coalitions],
+                                             dtype=np.uint64).view(np.int64)).to(dev)
+            self.model.init_params(self.glob, keys, self.stream)
+            _native.check(lib.mplc_cnn_copy_rows(_native.ptr(self.params), _native.ptr(self.glob), S,
+                                                 _native.ptr(src_map), R, self.stream), "mplc_cnn_copy_rows")
         self.rep_t = torch.from_numpy(self.rep_arr.view(np.uint8).copy()).to(dev)
         self.seq_t = torch.tensor(seq_recs, **i32) if seq_recs else None
         self.snap = None
@@ -395,7 +412,9 @@ class TrainBatch:
             # partner.model_weights of the aggregating variants: one snapshot row per (coalition, member)
             self.snap = torch.zeros((len(seq_recs) // SEQ_REC, S), **f32)
             self.snap_first_t = torch.tensor(snap_first, **i32)
+        self.resume_opt = resume["opt"] if resume is not None else None  # alloc() takes these rows over
         self.model.alloc(self)
+        self.resume_opt = None
         self.hstats = None
         if record:  # per-step training loss / accuracy sums of every replica (the head kernel's hstats)
             self.hstats = torch.zeros((R, 3), dtype=torch.float64, device=dev)
@@ -503,6 +522,13 @@ class TrainBatch:
         self.rep_t.copy_(torch.from_numpy(ra.view(np.uint8).copy()).to(self.dev))
         self.run_args = self.make_runs()
 
+    def release(self):
+        """Drop every device buffer of this batch (compaction: the live rows were gathered first)."""
+        self.params = self.glob = None
+        self.model.free(self)
+        self.ws = None
+        self.t = None
+
     def finalize(self):
         """Singleton final models -> their coalition rows; free training state."""
         import torch
@@ -530,9 +556,18 @@ class CnnBatchTrainer:
     def prepare(self, coalitions, epochs, record=False):
         return TrainBatch(self.eng, coalitions, epochs, self.lib, record=record)
 
+    # early stopping: once the replicas still training are at most this share of a lockstep batch, the batch is
+    # compacted (CnnBatchTrainer._compact); 0 keeps every batch whole
+    COMPACT_LIVE_SHARE = 0.75
+
     def run(self, coalitions, epochs, early_stopping, history=None, keep_models=False):
         """Train the coalitions in lockstep; returns (test accuracies, epochs done).  With `history` (a
-        dict, one coalition only) the learning history is recorded into it (HistoryRecorder)."""
+        dict, one coalition only) the learning history is recorded into it (HistoryRecorder).
+
+        Early stopping leaves stopped coalitions' replicas idle in the lockstep batch; when the live replicas
+        drop to COMPACT_LIVE_SHARE of the batch (FedAvg, several coalitions) the stopped coalitions' final models
+        are test-evaluated and the live ones continue in a smaller batch (_compact): same rows, optimizer state
+        and step schedule, so every v(S) is bit-identical to training without compaction."""
         eng = self.eng
         st = self.prepare(coalitions, epochs, record=history is not None)
         C = st.C
@@ -542,22 +577,41 @@ class CnnBatchTrainer:
                 raise ValueError("history recording takes exactly one coalition")
             rec = HistoryRecorder(self, st, epochs, history)
         sizes = eng.partner_sizes
-        fed = [ci for ci in range(C) if not st.coal_is_single[ci]]
         use_es = early_stopping and epochs > PATIENCE
+        share = float(getattr(eng, "compact_live_share", self.COMPACT_LIVE_SHARE))
+        compact = use_es and share > 0 and rec is None and not keep_models and not st.seq_mode
+        orig = list(range(C))  # this batch's coalition index -> the caller's
+        correct = np.zeros(C)
+        # per coalition (the caller's index): epochs done, the val losses the stopping rule compared, Keras
+        # EarlyStopping's best / wait
         epochs_done = np.full(C, epochs, dtype=np.int64)
-        val_hist = [[] for _ in range(C)]  # per coalition: the val losses the stopping rule compared
+        val_hist = [[] for _ in range(C)]
         es_best = np.full(C, np.inf)
         es_wait = np.zeros(C, dtype=np.int64)
-        spe = {ci: -(-sizes[coalitions[ci][0]] // eng.batch_sizes[coalitions[ci][0]])
-               for ci in range(C) if st.coal_is_single[ci]}
+
+        def layout(st):
+            fed = [ci for ci in range(st.C) if not st.coal_is_single[ci]]
+            spe = {ci: -(-sizes[st.coalitions[ci][0]] // eng.batch_sizes[st.coalitions[ci][0]])
+                   for ci in range(st.C) if st.coal_is_single[ci]}
+            return fed, spe
+        fed, spe = layout(st)
         per_epoch_fed = eng.minibatch_count * st.round_len
         progress = getattr(eng, "progress", None)
         stats = eng.stats
         for s in range(st.total_steps):
             # replica-steps launched, and those of replicas still training (early stopping leaves the stopped
-            # coalitions' replicas idle in the lockstep batch until it ends)
+            # coalitions' replicas idle in the lockstep batch until it ends or is compacted)
+            live_reps = int(np.sum(st.kind_host != REP_IDLE))
+            if compact and 0 < live_reps < st.R and live_reps <= share * st.R:
+                done = [ci for ci in range(st.C) if st.stopped[ci]]
+                live = [ci for ci in range(st.C) if not st.stopped[ci]]
+                correct[[orig[ci] for ci in done]] = self._final_correct(st, done)
+                st = self._compact(st, live)
+                orig = [orig[ci] for ci in live]
+                fed, spe = layout(st)
+                stats["compactions"] = stats.get("compactions", 0) + 1
             stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
-            stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(np.sum(st.kind_host != REP_IDLE))
+            stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + live_reps
             if progress is not None and s % 30 == 0:
                 progress(s, st.total_steps, st.R)
             if rec is not None and st.fed_steps and s % st.round_len == 0 and s < st.fed_steps:
@@ -568,7 +622,7 @@ class CnnBatchTrainer:
                 live = [ci for ci in fed if not st.stopped[ci]]
                 if live:  # val loss of each live global model at the start of epoch e (minibatch 0)
                     for ci, l in zip(live, self._val_loss(st.glob, live)):
-                        val_hist[ci].append(l)
+                        val_hist[orig[ci]].append(l)
             st.step(s)
             if rec is not None:
                 rec.after_step(s)
@@ -579,8 +633,9 @@ class CnnBatchTrainer:
                 if use_es and (s + 1) % per_epoch_fed == 0:
                     e = (s + 1) // per_epoch_fed - 1
                     for ci in fed:
-                        if not st.stopped[ci] and e >= PATIENCE and val_hist[ci][e] > val_hist[ci][e - PATIENCE]:
-                            epochs_done[ci] = e + 1
+                        h = val_hist[orig[ci]]
+                        if not st.stopped[ci] and e >= PATIENCE and h[e] > h[e - PATIENCE]:
+                            epochs_done[orig[ci]] = e + 1
                             st.stop(ci)
             if use_es and spe:
                 # singleton epoch ends: Keras EarlyStopping(monitor='val_loss', patience=10, min_delta=0)
@@ -589,13 +644,14 @@ class CnnBatchTrainer:
                 if ends:
                     for ci, l in zip(ends, self._val_loss(st.params, [st.coal_first[c] for c in ends])):
                         e = (s + 1) // spe[ci] - 1
-                        val_hist[ci].append(l)
-                        if l < es_best[ci]:
-                            es_best[ci], es_wait[ci] = l, 0
+                        o = orig[ci]
+                        val_hist[o].append(l)
+                        if l < es_best[o]:
+                            es_best[o], es_wait[o] = l, 0
                         else:
-                            es_wait[ci] += 1
-                            if es_wait[ci] >= PATIENCE:
-                                epochs_done[ci] = e + 1
+                            es_wait[o] += 1
+                            if es_wait[o] >= PATIENCE:
+                                epochs_done[o] = e + 1
                                 st.stop(ci)
             if st.stopped.all():
                 break
@@ -609,10 +665,35 @@ class CnnBatchTrainer:
             import torch
             torch.cuda.synchronize(eng.device)
             t0 = time.perf_counter()
-        correct, _ = self._evaluate(glob, list(range(C)), eng.x_test_d, eng.y_test_d)
+        c_end, _ = self._evaluate(glob, list(range(st.C)), eng.x_test_d, eng.y_test_d)
+        correct[orig] = c_end
         if getattr(eng, "time_test_eval", False):
             eng.stats["test_eval_s"] = eng.stats.get("test_eval_s", 0.0) + time.perf_counter() - t0
         return correct / float(eng.y_test_d.numel()), epochs_done
+
+    def _final_correct(self, st, cis):
+        """Test hits of the final models of stopped coalitions `cis` of batch `st` (a FedAvg coalition's model
+        is its coalition row, a singleton's its replica row)."""
+        import torch
+        rows = [st.params[st.coal_first[ci]] if st.coal_is_single[ci] else st.glob[ci] for ci in cis]
+        models = torch.stack(rows).contiguous()
+        correct, _ = self._evaluate(models, list(range(len(cis))), self.eng.x_test_d, self.eng.y_test_d)
+        return correct
+
+    def _compact(self, st, live):
+        """A batch of the live coalitions `live` of `st` continuing where `st` stands: their coalition rows,
+        replica rows and optimizer rows gathered in order, the same schedule geometry; `st` is released."""
+        import torch
+        dev = self.eng.device
+        reps = torch.tensor([r for ci in live for r in range(st.coal_first[ci], st.coal_first[ci + 1])],
+                            dtype=torch.int64, device=dev)
+        resume = {"glob": st.glob.index_select(0, torch.tensor(live, dtype=torch.int64, device=dev)),
+                  "params": st.params.index_select(0, reps),
+                  "opt": {k: v.index_select(0, reps) for k, v in st.model.opt_state(st).items()},
+                  "round_len": st.round_len, "fed_steps": st.fed_steps, "total_steps": st.total_steps}
+        coalitions, epochs = [st.coalitions[ci] for ci in live], st.epochs
+        st.release()
+        return TrainBatch(self.eng, coalitions, epochs, self.lib, resume=resume)
 
     # --------------------------------------------------------------------------------------------
     def _evaluate(self, params, rows, x, y):

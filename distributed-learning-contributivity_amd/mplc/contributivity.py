@@ -265,11 +265,15 @@ class Contributivity:
 
     def _frontier_plan(self, n, v_all, truncation):
         """plan(perms, stop) -> keys for one frontier step of a permutation wave (mplc.mc.plan_frontier): the
-        required first unknown prefixes plus speculative deeper prefixes up to `mc_plan_replicas` (default 1024)
-        replicas per rank, so that the lockstep batches stay large when few walks remain (config #4's
-        TMCS batches averaged 92 replicas).  mc_plan_replicas = 0 turns the speculation off."""
+        required first unknown prefixes plus the speculative deeper prefixes whose expected waste stays within one
+        batch's fixed cost (`mc_plan_overhead`, default 8 replica-trainings per rank), at most `mc_plan_replicas`
+        (default 4096) replicas per rank, so that the tail of a wave does not run as many tiny lockstep batches
+        (config #4's TMCS batches averaged 92 replicas).  mc_plan_replicas = 0 turns speculation off."""
         from .mc import plan_frontier, size_predictor
-        target = int(getattr(self.scenario, "mc_plan_replicas", 1024)) * self._world_size()
+        ws = self._world_size()
+        target = int(getattr(self.scenario, "mc_plan_replicas", 4096)) * ws
+        # a batch's fixed cost in replica-trainings; per rank the replicas are 1/ws of the batch
+        overhead = float(getattr(self.scenario, "mc_plan_overhead", 8.0)) * ws
         cache = self._cache()
         known = self.charac_fct_values
 
@@ -278,7 +282,7 @@ class Contributivity:
 
         def plan(perms, stop):
             pred = size_predictor(((k, v) for d in (cache, known) for k, v in d.items()), n, v_all)
-            keys, required = plan_frontier(perms, stop, value, pred, v_all, truncation, target)
+            keys, required = plan_frontier(perms, stop, value, pred, v_all, truncation, target, overhead)
             st = self.__dict__.setdefault("plan_stats", {"frontier_steps": 0, "required": 0, "speculative": 0})
             st["frontier_steps"] += 1
             st["required"] += required

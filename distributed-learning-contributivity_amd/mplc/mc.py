@@ -95,36 +95,59 @@ def mask_to_key(mask):
 
 
 def size_predictor(known, n, v_all):
-    """v(S) predicted from |S| alone (the speculative planner's truncation guess): per size the mean of the
-    known values of that size, linear in between, v_all at n.  known: iterable of (sorted key, value)."""
-    sums = np.zeros(n + 1)
-    cnt = np.zeros(n + 1)
+    """v(S) predicted from |S| alone (the speculative planner's truncation model): per size the mean and standard
+    deviation of the known values of that size, linear in between, v_all at n.  known: iterable of (key, value).
+    Returns (mean[n + 1], sd[n + 1])."""
+    vals = [[] for _ in range(n + 1)]
     for k, v in known:
         if 0 < len(k) < n:
-            sums[len(k)] += v
-            cnt[len(k)] += 1
-    sums[n], cnt[n] = v_all, 1
-    xs = [s for s in range(1, n + 1) if cnt[s] > 0]
-    return np.interp(np.arange(n + 1), xs, [sums[s] / cnt[s] for s in xs])
+            vals[len(k)].append(v)
+    vals[n] = [v_all]
+    xs = [s for s in range(1, n + 1) if vals[s]]
+    mean = np.interp(np.arange(n + 1), xs, [float(np.mean(vals[s])) for s in xs])
+    # a size's own spread once it has enough values, else the spread of everything known (never overconfident:
+    # an underestimated spread makes the planner speculate past truncations it did not expect)
+    pooled = [v for s in range(1, n) for v in vals[s]]
+    prior = float(np.std(pooled)) if len(pooled) > 1 else 0.1
+    sx = [s for s in range(1, n) if len(vals[s]) >= 10]
+    sd = np.interp(np.arange(n + 1), sx, [float(np.std(vals[s])) for s in sx]) if sx else np.full(n + 1, prior)
+    sd = np.where([len(vals[s]) >= 10 for s in range(n + 1)], sd, np.maximum(sd, prior))
+    return mean, np.maximum(sd, 0.005)
 
 
-def plan_frontier(perms, stop, value, pred, v_all, truncation, target_replicas, margin=0.5):
+def _p_continue(v, mean, sd, v_all, truncation):
+    """Probability that a walk continues past a prefix (its truncation test |v_all - v(prefix)| < truncation does
+    not fire): exact for a known value v, else with v ~ N(mean, sd)."""
+    if v is not None:
+        return 0.0 if abs(v_all - v) < truncation else 1.0
+    from scipy.stats import norm
+    hit = norm.cdf((v_all + truncation - mean) / sd) - norm.cdf((v_all - truncation - mean) / sd)
+    return float(1.0 - hit)
+
+
+def plan_frontier(perms, stop, value, pred, v_all, truncation, target_replicas, overhead_replicas=16.0):
     """The coalitions to train for one frontier step of a wave of truncated permutation walks
     (mplc/contributivity.py:215-246: a walk needs v(perm[:j+1]) while |v_all - v(perm[:j])| >= truncation).
 
     perms [K][n]; stop[k] = position j of walk k's first unknown prefix perm[:j+1] (n: the walk is complete).
-    Every first unknown prefix is REQUIRED.  While the batch holds fewer than `target_replicas` replicas (one per
-    member), deeper prefixes of the same walks are added level by level as SPECULATION: the walk reaches
-    perm[:j+2] unless its truncation test fires on perm[:j+1] - decided exactly when that value is known, else
-    guessed from pred[|S|] (size_predictor) with the band widened by `margin`.  Speculation never changes a
-    result (v(S) is a function of (S, seed) only, and the sequential loop still decides what it asks for): a
-    wrong guess costs the training of a coalition the loop will not use.
-    value(key) -> known v or None.  Returns (keys, number of required keys); keys are sorted tuples."""
+    Every first unknown prefix is REQUIRED.  Deeper prefixes of the same walks are added as SPECULATION, most
+    probable first: the walk reaches perm[:j+2] only if its truncation test does not fire on perm[:j+1] - certain
+    when that value is known, else modelled from the known values of the same size (pred = size_predictor).  Each
+    speculative coalition S that the walks then do not need costs |S| replica-trainings; each frontier step saved
+    costs a lockstep batch's fixed overhead, about `overhead_replicas` replica-trainings (CIFAR10 on one MI355X:
+    59 ms per batch vs 3.5 ms per replica, scripts/sim_tmcs_planning.py).  So speculation stops once the expected
+    waste sum (1 - p) |S| would exceed that overhead, or the batch holds `target_replicas` replicas.  In the bulk of
+    a wave (many walks, a level is worth many batches' overhead) little is speculated; in its tail (few walks)
+    whole chains are.  Speculation never changes a result (v(S) is a function of (S, seed) only, and the
+    sequential loop still decides what it asks for).  value(key) -> known v or None.
+    Returns (keys, number of required keys); keys are sorted tuples."""
+    import heapq
     perms = np.asarray(perms)
     K, n = perms.shape
+    mean, sd = pred
     chosen = {}
     replicas = 0
-    chains = []
+    heap = []  # (-p_reach of the chain's next prefix, walk, position of the last chosen prefix)
     for k in range(K):
         j = int(stop[k])
         if j >= n:
@@ -133,26 +156,27 @@ def plan_frontier(perms, stop, value, pred, v_all, truncation, target_replicas, 
         if key not in chosen:
             chosen[key] = True
             replicas += len(key)
-        chains.append((k, j))
+        heap.append((-1.0, k, j))
     required = len(chosen)
-    while chains and replicas < target_replicas:
-        deeper = []
-        for k, j in chains:
-            if j + 1 >= n:
-                continue
-            prev = tuple(sorted(int(i) for i in perms[k, :j + 1]))
-            v = value(prev)
-            if v is not None:
-                if abs(v_all - v) < truncation:
-                    continue  # the walk truncates after prev: nothing deeper is ever asked for
-            elif abs(v_all - pred[j + 1]) < truncation * (1.0 + margin):
-                continue  # likely to truncate there: do not speculate past it
-            key = tuple(sorted(int(i) for i in perms[k, :j + 2]))
-            if key not in chosen and value(key) is None:
-                chosen[key] = True
-                replicas += len(key)
-            deeper.append((k, j + 1))
-        chains = deeper
+    heapq.heapify(heap)
+    waste = 0.0
+    while heap and replicas < target_replicas:
+        negp, k, j = heapq.heappop(heap)
+        if j + 1 >= n:
+            continue
+        prev = tuple(sorted(int(i) for i in perms[k, :j + 1]))
+        p = -negp * _p_continue(value(prev), mean[j + 1], sd[j + 1], v_all, truncation)
+        if p <= 0.0:
+            continue
+        key = tuple(sorted(int(i) for i in perms[k, :j + 2]))
+        if key not in chosen and value(key) is None:
+            cost = (1.0 - p) * len(key)
+            if waste + cost > overhead_replicas:
+                continue  # not worth a batch's overhead; shallower prefixes of other walks may still be
+            waste += cost
+            chosen[key] = True
+            replicas += len(key)
+        heapq.heappush(heap, (-p, k, j + 1))
     return list(chosen), required
 
 

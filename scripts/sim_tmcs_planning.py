@@ -44,7 +44,7 @@ def load_table(path, n):
     return value, len(vals)
 
 
-def run(n, value, method, target, wave_scale=1, adaptive=True):
+def run(n, value, method, target, wave_scale=1, adaptive=True, margin=0.5):
     batches = []
 
     class Approach:
@@ -57,7 +57,8 @@ def run(n, value, method, target, wave_scale=1, adaptive=True):
 
     partners = [types.SimpleNamespace(id=i, y_train=np.zeros(1822)) for i in range(n)]
     sc = types.SimpleNamespace(partners_list=partners, multi_partner_learning_approach=Approach, mc_plan_replicas=target,
-                               mc_wave_scale=wave_scale, mc_wave_adaptive=adaptive)
+                               mc_wave_scale=wave_scale, mc_wave_adaptive=adaptive,
+                               mc_plan_overhead=margin)
     np.random.seed(0)
     c = Contributivity(scenario=sc)
     c.compute_contributivity(method)
@@ -71,19 +72,21 @@ def main():
     ap.add_argument("--n", type=int, default=20)
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--targets", default="0,256,512,1024,2048,4096")
+    ap.add_argument("--margins", default="16", help="mc_plan_overhead values")
     ap.add_argument("--cost", default="0.09,0.0033", help="A,B of the per-batch time model (s, s per replica)")
     args = ap.parse_args()
     A, B = (float(x) for x in args.cost.split(","))
     value, held = load_table(args.values, args.n)
     ref = None
-    for target, adaptive in [(int(t), a) for a in (False, True) for t in args.targets.split(",")]:
-        c, batches, trained = run(args.n, value, args.method, target, adaptive=adaptive)
+    for target, adaptive, margin in [(int(t), a, float(m)) for a in (False, True) for t in args.targets.split(",")
+                                     for m in args.margins.split(",")]:
+        c, batches, trained = run(args.n, value, args.method, target, adaptive=adaptive, margin=margin)
         if ref is None:
             ref = c.contributivity_scores
         assert np.array_equal(ref, c.contributivity_scores)  # speculation never changes the result
         reps = np.array(batches)
         est = len(reps) * A + reps.sum() * B
-        print(f"{'adaptive' if adaptive else 'fixed   '} target {target:5d}: batches {len(reps):4d}  replicas/batch {reps.mean():7.1f} (median "
+        print(f"{'adaptive' if adaptive else 'fixed   '} target {target:5d} overhead {margin}: batches {len(reps):4d}  replicas/batch {reps.mean():7.1f} (median "
               f"{np.median(reps):6.0f})  counted {c.first_charac_fct_calls_count}  trained {trained}  "
               f"(+{100 * (trained / c.first_charac_fct_calls_count - 1):.1f} %)  replicas {reps.sum()}  "
               f"est {est:6.1f} s -> {c.first_charac_fct_calls_count / est:6.1f} evals/s  "
