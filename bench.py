@@ -481,6 +481,8 @@ def bench_train(args, rank, world):
     from mplc.engine import CoalitionEngine
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
+    if args.compact_share is not None:  # early-stopping batch compaction threshold (0: off; mplc/cnn.py)
+        eng.compact_live_share = args.compact_share
     eng.warmup()  # untimed: code-object load (no training launch, so rocprof averages = timed launches)
 
     def progress(s, total, R):  # heartbeat for long sweeps (E=40: one sweep is several minutes)
@@ -593,6 +595,9 @@ def bench_train(args, rank, world):
             "val_eval_share": round(st_.get("es_val_s", 0.0) / max(1e-9, (steps + warm) * ms_per_step / 1000), 4),
             "replica_steps_idle_share": round(1 - st_.get("replica_steps_live", 0) / max(1, st_.get("replica_steps", 1)),
                                               4),
+            "replica_steps": int(st_.get("replica_steps", 0)), "replica_steps_live": int(st_.get("replica_steps_live", 0)),
+            "compactions": int(st_.get("compactions", 0)),
+            "compact_live_share": float(getattr(eng, "compact_live_share", eng.trainer.COMPACT_LIVE_SHARE)),
             "data": f"learnable synthetic MNIST (class templates, signal {args.mnist_signal})"}
         out["epochs_per_coalition"] = None
         out["config"]["workload"] = out["config"]["workload"].replace(f"E={args.epochs} fixed",
@@ -829,6 +834,8 @@ def main():
                     help="train leg at the reference's stopping rule (with --epochs 40: its defaults)")
     ap.add_argument("--mnist-signal", type=float, default=0.0,
                     help="class-template signal of the synthetic MNIST (0: random labels)")
+    ap.add_argument("--compact-share", type=float, default=None,
+                    help="train leg: early-stopping batch compaction threshold (default mplc/cnn.py; 0 = off)")
     ap.add_argument("--dump-values", default=None, help="cifar leg: save the trained v(S) values (npz) here")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")

@@ -1599,7 +1599,10 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 // fresh optimizer's first step).
 // ------------------------------------------------------------------------------------------------
 constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
-constexpr int D5_GROUPS = 4;    // row groups per block
+#ifndef MPLC_D5_GROUPS
+#define MPLC_D5_GROUPS 4
+#endif
+constexpr int D5_GROUPS = MPLC_D5_GROUPS;  // row groups per block
 constexpr int D5_SCHUNK = 16;   // samples staged at a time
 
 __global__ __launch_bounds__(256) void dense5_bwd_kernel(
