@@ -475,7 +475,10 @@ __device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) 
 // U[xi][cin][cout] = (G g G^T)[i][j], xi = 4i + j, for the kernel g of channel pair (cin, cout):
 // FLIP = 0: the layer's forward kernel, g[ky][kx] = W[ky][kx][cin][cout];
 // FLIP = 1: the data gradient's kernel, g[ky][kx] = W[2 - ky][2 - kx][cout][cin] (in = the layer's co).
-template <int CIN, int COUT, int FLIP>
+// XIL = 1 (the layout the convolution kernels read) stores the pair's 16 transform points contiguously,
+// U[cin][cout][xi]: a wave-local lane reads its 16 B operands of a k-step as 4 x 16 B, a row-per-wave lane its 4 as
+// one 16-B load (instead of 16 / 4 scalar loads); XIL = 0 the transform point first, U[xi][cin][cout].
+template <int CIN, int COUT, int FLIP, int XIL = 0>
 __device__ __forceinline__ void wino_u_pair(const float* __restrict__ W, float* __restrict__ U, int e) {
   const int cin = e / COUT, cout = e % COUT;
   float g[3][3];
@@ -498,8 +501,12 @@ __device__ __forceinline__ void wino_u_pair(const float* __restrict__ W, float* 
   for (int i = 0; i < 4; ++i) {
     float o[4];
     wino_g_rows(gg[i], o);
+    if (XIL) {
+      reinterpret_cast<fvec4*>(U + (int64_t)e * 16)[i] = fvec4{o[0], o[1], o[2], o[3]};
+    } else {
 #pragma unroll
-    for (int jx = 0; jx < 4; ++jx) U[(4 * i + jx) * CIN * COUT + e] = o[jx];
+      for (int jx = 0; jx < 4; ++jx) U[(4 * i + jx) * CIN * COUT + e] = o[jx];
+    }
   }
 }
 
@@ -511,7 +518,7 @@ static_assert(WU_4 + 16 * 64 * 64 == MPLC_CIFAR_WT, "MPLC_CIFAR_WT must hold con
 // The data gradient's kernel (FLIP = 1) reads W transposed, W[k][cout][cin]: one thread per channel pair in
 // U's order would read with a stride of CIN floats, so a block takes a 16 x 16 (cin, cout) tile, reads it
 // cin-fastest, transforms it and writes U cout-fastest through an LDS transpose (same arithmetic per pair).
-template <int CIN, int COUT>
+template <int CIN, int COUT, int XIL = 0>
 __device__ __forceinline__ void wino_u_tile_flip(const float* __restrict__ W, float* __restrict__ U, int tile,
                                                  float (*sx)[16 * 17]) {
   const int tid = threadIdx.x;
@@ -540,6 +547,15 @@ __device__ __forceinline__ void wino_u_tile_flip(const float* __restrict__ W, fl
   }
   __syncthreads();
   const int wcin = cin0 + (tid >> 4), wcout = cout0 + (tid & 15);  // write order: cout fastest
+  if (XIL) {  // the pair's 16 points contiguous (U[cin][cout][xi])
+    fvec4* u4 = reinterpret_cast<fvec4*>(U + (int64_t)(wcin * COUT + wcout) * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = (tid >> 4) * 17 + (tid & 15);
+      u4[i] = fvec4{sx[4 * i][c], sx[4 * i + 1][c], sx[4 * i + 2][c], sx[4 * i + 3][c]};
+    }
+    return;
+  }
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi) U[xi * CIN * COUT + wcin * COUT + wcout] = sx[xi][(tid >> 4) * 17 + (tid & 15)];
 }
@@ -554,19 +570,19 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   if (FLIP) {  // 16 x 16 tiles: conv2 4 | conv3 8 | conv4 16 (the grid's 28 blocks per replica)
     __shared__ float sx[16][16 * 17];
     const int b = blockIdx.x;
-    if (b < 4) wino_u_tile_flip<32, 32>(P + OFF_W2, Ur + WU_2, b, sx);
-    else if (b < 12) wino_u_tile_flip<64, 32>(P + OFF_W3, Ur + WU_3, b - 4, sx);  // dgrad: in = conv3's 64 co
-    else if (b < 28) wino_u_tile_flip<64, 64>(P + OFF_W4, Ur + WU_4, b - 12, sx);
+    if (b < 4) wino_u_tile_flip<32, 32, 1>(P + OFF_W2, Ur + WU_2, b, sx);
+    else if (b < 12) wino_u_tile_flip<64, 32, 1>(P + OFF_W3, Ur + WU_3, b - 4, sx);  // dgrad: in = conv3's 64 co
+    else if (b < 28) wino_u_tile_flip<64, 64, 1>(P + OFF_W4, Ur + WU_4, b - 12, sx);
     return;
   }
   const int e = blockIdx.x * 256 + threadIdx.x;  // pair index over conv2 (1024) | conv3 (2048) | conv4 (4096)
   if (e < 1024) {
-    wino_u_pair<32, 32, FLIP>(P + OFF_W2, Ur + WU_2, e);
+    wino_u_pair<32, 32, FLIP, 1>(P + OFF_W2, Ur + WU_2, e);
   } else if (e < 3072) {
-    if (FLIP) wino_u_pair<64, 32, 1>(P + OFF_W3, Ur + WU_3, e - 1024);   // dgrad: in = conv3's 64 co
-    else wino_u_pair<32, 64, 0>(P + OFF_W3, Ur + WU_3, e - 1024);
+    if (FLIP) wino_u_pair<64, 32, 1, 1>(P + OFF_W3, Ur + WU_3, e - 1024);   // dgrad: in = conv3's 64 co
+    else wino_u_pair<32, 64, 0, 1>(P + OFF_W3, Ur + WU_3, e - 1024);
   } else if (e < 7168) {
-    wino_u_pair<64, 64, FLIP>(P + OFF_W4, Ur + WU_4, e - 3072);
+    wino_u_pair<64, 64, FLIP, 1>(P + OFF_W4, Ur + WU_4, e - 3072);
   }
 }
 
@@ -637,12 +653,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float sa = (wi == 2) ? -1.0f : 1.0f;
   const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
   const int drow = (rb - ra) * ROWP;
-  const float* Ub = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + kq * CO + tl;
+  // B operands of k-step st: U[4 st + kq][16 cg + tl][4 wi + jj] (wino_u_kernel's xi-last layout): the wave's
+  // 4 transform points of one channel pair are one 16-B load
+  const fvec4* Ub = reinterpret_cast<const fvec4*>(a.w + (int64_t)r * a.w_rstride) + (kq * CO + tl) * 4 + wi;
   auto load_b = [&](int st, float (&bv)[4 * NCG]) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-      for (int cg = 0; cg < NCG; ++cg) bv[NCG * jj + cg] = Ub[(int64_t)jj * CI * CO + (4 * st) * CO + 16 * cg];
+    for (int cg = 0; cg < NCG; ++cg) {
+      const fvec4 u = Ub[((4 * st) * CO + 16 * cg) * 4];
+      bv[NCG * 0 + cg] = u.x;
+      bv[NCG * 1 + cg] = u.y;
+      bv[NCG * 2 + cg] = u.z;
+      bv[NCG * 3 + cg] = u.w;
+    }
   };
   float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
   const float* bias = (EPI == EPI_FWD || POOL) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
@@ -1042,13 +1064,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int tl = lane & 15, kq = lane >> 4;
   const int tile = min(16 * wave + tl, ntile - 1);
   const float* dpa = in_s + ((2 * (tile / TXT)) * LC + 2 * (tile % TXT)) * CIP + kq;
-  // B operands of k-step st: U[xi][4 st + kq][16 cg + tl], 16 xi x 2 cg
-  const float* Ub = a.w + (int64_t)r * a.w_rstride + kq * CO + tl;
+  // B operands of k-step st: U[4 st + kq][16 cg + tl][xi] (the xi-last layout of wino_u_kernel's conv2 section):
+  // a lane's 16 transform points of one channel pair are 64 contiguous bytes, 4 x 16-B loads per cg
+  const fvec4* Ub = reinterpret_cast<const fvec4*>(a.w + (int64_t)r * a.w_rstride) + (kq * CO + tl) * 4;
   auto load_b = [&](int st, float (&bv)[32]) {
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi)
+    for (int cg = 0; cg < 2; ++cg)
 #pragma unroll
-      for (int cg = 0; cg < 2; ++cg) bv[2 * xi + cg] = Ub[(int64_t)xi * CI * CO + (4 * st) * CO + 16 * cg];
+      for (int q = 0; q < 4; ++q) {
+        const fvec4 u = Ub[((4 * st) * CO + 16 * cg) * 4 + q];
+        bv[2 * (4 * q + 0) + cg] = u.x;
+        bv[2 * (4 * q + 1) + cg] = u.y;
+        bv[2 * (4 * q + 2) + cg] = u.z;
+        bv[2 * (4 * q + 3) + cg] = u.w;
+      }
   };
   fvec4 acc[16][2];
 #pragma unroll
@@ -1603,7 +1632,10 @@ constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
 #define MPLC_D5_GROUPS 4
 #endif
 constexpr int D5_GROUPS = MPLC_D5_GROUPS;  // row groups per block
-constexpr int D5_SCHUNK = 16;   // samples staged at a time
+#ifndef MPLC_D5_SCHUNK
+#define MPLC_D5_SCHUNK 16
+#endif
+constexpr int D5_SCHUNK = MPLC_D5_SCHUNK;  // samples staged at a time
 
 __global__ __launch_bounds__(256) void dense5_bwd_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
@@ -1798,19 +1830,13 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------------
 #define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
 // Winograd F(2x2,3x3): <HI, WI, CI, CO, PAD, tile rows per band, EPI>; bands = ceil(tile rows / BTY)
-#ifdef CIFAR_WINO_ROWS  // build switch: the row-per-wave form for the CO = 32 layers too (A/B)
-#define CONV2_FWD wino_kernel<32, 32, 32, 32, 0, 4, EPI_FWD_POOL>     /* 15x15 windows, 4 bands, 59.2 KB */
-#define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL> /* 8x8 tiles,    2 bands, 63.7 KB */
-#define CONV2_DGRAD wino_kernel<30, 30, 32, 32, 2, 4, EPI_BWD_MASK>   /* 16x16 tiles,  4 bands, 61.8 KB */
-#define CONV3_DGRAD_NT 256
-#else  // wave-local form: <HI, WI, CI, CO, PAD, BTY, waves, EPI>
+// wave-local form: <HI, WI, CI, CO, PAD, BTY, waves, EPI>; reads conv2's Winograd weights in the xi-last layout
 #define CONV2_FWD wino_wl_kernel<32, 32, 32, 32, 0, 4, 4, EPI_FWD_POOL>      /* 60 tiles, 4 bands, 42 KB */
 // conv3's data gradient keeps the row form: its bands hold 2 tile groups, and the wave-local form with 2-wave
 // blocks measured slower (4585 vs 4264 ms over a config #4 run, profiles/r03_driver_bench_v2.json)
 #define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL>        /* 8x8 tiles, 2 bands, 63.7 KB */
 #define CONV2_DGRAD wino_wl_kernel<30, 30, 32, 32, 2, 4, 4, EPI_BWD_MASK>    /* 64 tiles, 4 bands, 44.9 KB */
 #define CONV3_DGRAD_NT 256
-#endif
 #define CONV3_FWD wino_kernel<15, 15, 32, 64, 1, 8, EPI_FWD>          /* 8x8 tiles,    1 band,  59.7 KB */
 #define CONV4_FWD wino_kernel<15, 15, 64, 64, 0, 6, EPI_FWD_POOL>     /* 6x6 windows,  1 band,  67.9 KB */
 #define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK>   /* 8x8 tiles,    2 bands, 63.7 KB */

@@ -978,10 +978,13 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           const float v = (c & 0x80) ? pdv[s] : 0.0f;
           const int sel = c & 3;
           float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
-          d[0] = (sel == 0) ? v : 0.0f;
-          d[BWD_CS] = (sel == 1) ? v : 0.0f;
-          d[BWD_DC * BWD_CS] = (sel == 2) ? v : 0.0f;
-          d[BWD_DC * BWD_CS + BWD_CS] = (sel == 3) ? v : 0.0f;
+          // the window's 4 pixels zeroed, then the value at the argmax (same thread, same address: in order): no
+          // per-pixel compare / select chain (SGPR-mask hazards padded with s_nop in every one)
+          d[0] = 0.0f;
+          d[BWD_CS] = 0.0f;
+          d[BWD_DC * BWD_CS] = 0.0f;
+          d[BWD_DC * BWD_CS + BWD_CS] = 0.0f;
+          d[(sel >> 1) * (BWD_DC * BWD_CS) + (sel & 1) * BWD_CS] = v;
         }
       }
 #endif
