@@ -475,9 +475,10 @@ __device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) 
 // U[xi][cin][cout] = (G g G^T)[i][j], xi = 4i + j, for the kernel g of channel pair (cin, cout):
 // FLIP = 0: the layer's forward kernel, g[ky][kx] = W[ky][kx][cin][cout];
 // FLIP = 1: the data gradient's kernel, g[ky][kx] = W[2 - ky][2 - kx][cout][cin] (in = the layer's co).
-// XIL = 1 (the layout the convolution kernels read) stores the pair's 16 transform points contiguously,
-// U[cin][cout][xi]: a wave-local lane reads its 16 B operands of a k-step as 4 x 16 B, a row-per-wave lane its 4 as
-// one 16-B load (instead of 16 / 4 scalar loads); XIL = 0 the transform point first, U[xi][cin][cout].
+// XIL = 1 stores the pair's 16 transform points contiguously, U[cin][cout][xi] (conv2: the wave-local kernel reads a
+// lane's 16 B operands of a k-step as 4 x 16 B instead of 16 scalar loads: conv2 forward -5 %); XIL = 0 the
+// transform point first, U[xi][cin][cout] (conv3 / conv4: the row-per-wave kernel reads 4 of the 16 points per
+// pair, coalesced across the lanes in this layout).
 template <int CIN, int COUT, int FLIP, int XIL = 0>
 __device__ __forceinline__ void wino_u_pair(const float* __restrict__ W, float* __restrict__ U, int e) {
   const int cin = e / COUT, cout = e % COUT;
@@ -571,18 +572,18 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
     __shared__ float sx[16][16 * 17];
     const int b = blockIdx.x;
     if (b < 4) wino_u_tile_flip<32, 32, 1>(P + OFF_W2, Ur + WU_2, b, sx);
-    else if (b < 12) wino_u_tile_flip<64, 32, 1>(P + OFF_W3, Ur + WU_3, b - 4, sx);  // dgrad: in = conv3's 64 co
-    else if (b < 28) wino_u_tile_flip<64, 64, 1>(P + OFF_W4, Ur + WU_4, b - 12, sx);
+    else if (b < 12) wino_u_tile_flip<64, 32>(P + OFF_W3, Ur + WU_3, b - 4, sx);  // dgrad: in = conv3's 64 co
+    else if (b < 28) wino_u_tile_flip<64, 64>(P + OFF_W4, Ur + WU_4, b - 12, sx);
     return;
   }
   const int e = blockIdx.x * 256 + threadIdx.x;  // pair index over conv2 (1024) | conv3 (2048) | conv4 (4096)
   if (e < 1024) {
     wino_u_pair<32, 32, FLIP, 1>(P + OFF_W2, Ur + WU_2, e);
   } else if (e < 3072) {
-    if (FLIP) wino_u_pair<64, 32, 1, 1>(P + OFF_W3, Ur + WU_3, e - 1024);   // dgrad: in = conv3's 64 co
-    else wino_u_pair<32, 64, 0, 1>(P + OFF_W3, Ur + WU_3, e - 1024);
+    if (FLIP) wino_u_pair<64, 32, 1>(P + OFF_W3, Ur + WU_3, e - 1024);   // dgrad: in = conv3's 64 co
+    else wino_u_pair<32, 64, 0>(P + OFF_W3, Ur + WU_3, e - 1024);
   } else if (e < 7168) {
-    wino_u_pair<64, 64, FLIP, 1>(P + OFF_W4, Ur + WU_4, e - 3072);
+    wino_u_pair<64, 64, FLIP>(P + OFF_W4, Ur + WU_4, e - 3072);
   }
 }
 
@@ -653,18 +654,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float sa = (wi == 2) ? -1.0f : 1.0f;
   const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
   const int drow = (rb - ra) * ROWP;
-  // B operands of k-step st: U[4 st + kq][16 cg + tl][4 wi + jj] (wino_u_kernel's xi-last layout): the wave's
-  // 4 transform points of one channel pair are one 16-B load
-  const fvec4* Ub = reinterpret_cast<const fvec4*>(a.w + (int64_t)r * a.w_rstride) + (kq * CO + tl) * 4 + wi;
+  // B operands of k-step st: U[4 wi + jj][4 st + kq][16 cg + tl] (the xi-first layout: a 16-lane group reads 64
+  // contiguous bytes per transform point; the xi-last layout's one 16-B load per channel pair measured 5-10 % slower
+  // here, scripts/r04/gpu_ab_cifar.sh)
+  const float* Ub = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + kq * CO + tl;
   auto load_b = [&](int st, float (&bv)[4 * NCG]) {
 #pragma unroll
-    for (int cg = 0; cg < NCG; ++cg) {
-      const fvec4 u = Ub[((4 * st) * CO + 16 * cg) * 4];
-      bv[NCG * 0 + cg] = u.x;
-      bv[NCG * 1 + cg] = u.y;
-      bv[NCG * 2 + cg] = u.z;
-      bv[NCG * 3 + cg] = u.w;
-    }
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int cg = 0; cg < NCG; ++cg) bv[NCG * jj + cg] = Ub[(int64_t)jj * CI * CO + (4 * st) * CO + 16 * cg];
   };
   float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
   const float* bias = (EPI == EPI_FWD || POOL) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
