@@ -1160,257 +1160,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// conv_bwd_data, LDS-DMA form (MPLC_BWD_DMA): the same GEMM, epilogue and arithmetic as conv_bwd_data_kernel
-// (bit-identical results), but its two operand streams arrive by global_load_lds_dwordx4, double-buffered so that
-// the next stage's copy runs during the current stage's MFMAs instead of in a staging phase of its own:
-//   - Ur in eighths of 8 output channels (2 k-steps, 16 KB, the quarter layout's XOR swizzle applied through the
-//     source address: an LDS-DMA destination is lane-linear), the next eighth copied during this eighth's k-steps;
-//   - dZ2 as the raw (dp, code) pairs of a quarter of the channels (84 windows x 16 channels: 5.4 KB of values,
-//     1.3 KB of codes), the next quarter's copied during this quarter: no dense un-pooled band at all - a lane
-//     builds its tile's 4x4 patch from the 4 pooling windows it covers (one value each, at the window's argmax).
-// One barrier per eighth (its DMA landed everywhere and every wave is done with the buffer the next DMA refills).
-// LDS 54.5 KB per block, in one array (a second __shared__ object can make hipcc wait for the DMA at every LDS
-// read, cdna_hip_programming.md 5, trap 4a).
-// ------------------------------------------------------------------------------------------------
-#define LDS_AS __attribute__((address_space(3)))
-#define GLB_AS __attribute__((address_space(1)))
-constexpr int BD_EIGHTH = 8 * C1 * 16;       // Ur floats of 8 output channels [co 8][ci 32][xi 16]
-constexpr int BD_WIN = BWD_WR * PL;          // the band's 84 pooling windows (7 rows x 12)
-constexpr int BD_PV = BD_WIN * 16;           // a quarter's dp values [window][16 channels]
-constexpr int BD_PCF = BD_WIN * 16 / 4;      // its codes [window][16] bytes, in floats
-constexpr int BD_UR0 = 0, BD_UR1 = BD_EIGHTH, BD_PV0 = 2 * BD_EIGHTH, BD_PV1 = BD_PV0 + BD_PV,
-              BD_PC0 = BD_PV1 + BD_PV, BD_PC1 = BD_PC0 + BD_PCF, BD_IMG = BD_PC1 + BD_PCF,
-              BD_RED = BD_IMG + IMG * IMG, BD_LDS = BD_RED + 4 * 10 * 32;
-static_assert(BD_PV0 % 4 == 0 && BD_PV1 % 4 == 0 && BD_PC0 % 4 == 0 && BD_PC1 % 4 == 0, "16-B DMA destinations");
-static_assert(BD_EIGHTH / 4 == 4 * BWD_THREADS, "an eighth of Ur = 4 DMA chunks per thread");
-
-__device__ __forceinline__ void glds16(const void* g, float* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds_wave_base, 16, 0, 0);
-}
-
-__global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_bwd_data_dma_kernel(
-    const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
-    const float* __restrict__ params, int64_t stride, const float* __restrict__ Ur,
-    const float* __restrict__ dPool, const uint8_t* __restrict__ code, float* __restrict__ w1_part) {
-  __shared__ __attribute__((aligned(16))) float lds[BD_LDS];
-  const int64_t lb = xcd_block();  // logical block (band, sample, r), replica-major
-  const int band = (int)(lb % BWD_BANDS);
-  const int j = (int)((lb / BWD_BANDS) % gridDim.y);
-  const int r = (int)(lb / ((int64_t)BWD_BANDS * gridDim.y));
-  if (j >= cnt[r]) return;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int tl = lane & 15, kq = lane >> 4;
-  const float* P = params + (int64_t)r * stride;
-  const int tile0 = band * BWD_BAND_TILES;
-  const int ty0 = tile0 / 13;
-  const int wy0 = ty0 - 1;  // first window row of the band (local window row 0)
-  const int gt0 = tile0 + 16 * wave;
-  const bool active = gt0 < BWD_TILES;
-  const float* Urr = Ur + (int64_t)r * MPLC_CNN_W2T;
-  const float* dps = dPool + ((int64_t)r * bmax + j) * FEAT;
-  const uint8_t* cds = code + ((int64_t)r * bmax + j) * FEAT;
-  // ---- LDS-DMA issue (every thread; lanes with nothing to copy are masked, the wave's LDS base is uniform)
-  auto dma_ur = [&](int e, int buf) {  // eighth e of Ur into buffer buf; dest chunk d holds source chunk
-#pragma unroll                          //   pair * 4 + ((d & 3) ^ swz(pair)) (the quarter kernel's swizzle)
-    for (int k = 0; k < 4; ++k) {
-      const int d = k * BWD_THREADS + tid;
-      const int pair = d >> 2, m = (d & 3) ^ ((pair >> 2) & 3);
-      glds16(Urr + e * BD_EIGHTH + (pair * 4 + m) * 4, lds + (buf ? BD_UR1 : BD_UR0) + (k * BWD_THREADS + 64 * wave) * 4);
-    }
-  };
-  auto dma_pairs = [&](int q, int buf) {  // quarter q's (dp, code) of the band's valid windows
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {  // dp: chunk c = window * 4 + part (4 channels), 336 chunks
-      const int c = k * BWD_THREADS + tid;
-      const int w = c >> 2, wy = wy0 + w / PL;
-      if (c < BD_WIN * 4 && wy >= 0 && wy < PL)
-        glds16(dps + (wy * PL + w % PL) * C2 + 16 * q + 4 * (c & 3),
-               lds + (buf ? BD_PV1 : BD_PV0) + (k * BWD_THREADS + 64 * wave) * 4);
-    }
-    {  // codes: chunk c = window (16 channels), 84 chunks
-      const int wy = wy0 + tid / PL;
-      if (tid < BD_WIN && wy >= 0 && wy < PL)
-        glds16(cds + (wy * PL + tid % PL) * C2 + 16 * q, lds + (buf ? BD_PC1 : BD_PC0) + 64 * wave * 4);
-    }
-  };
-  dma_ur(0, 0);
-  dma_pairs(0, 0);
-  {  // the sample's image (conv1 recompute in the epilogue)
-    const float* xr = x + (int64_t)idx[(int64_t)r * bmax + j] * IMG * IMG;
-    for (int e = tid; e < IMG * IMG; e += BWD_THREADS) lds[BD_IMG + e] = xr[e];
-  }
-  // A operand: this lane's tile and the 4 pooling windows its 4x4 patch covers (a, b = window row / column within
-  // the patch); windows outside the 12 x 12 grid contribute zeros (their pairs are never copied)
-  const int tcl = min(gt0 + tl, BWD_TILES - 1);
-  const int ty = tcl / 13, tx = tcl % 13;
-  int woff[2][2];
-  bool wval[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int wy = ty - 1 + a, wx = tx - 1 + b;
-      wval[a][b] = wy >= 0 && wy < PL && wx >= 0 && wx < PL;
-      woff[a][b] = wval[a][b] ? ((wy - wy0) * PL + wx) * 16 : 0;
-    }
-  const int swz = (tl >> 2) & 3;
-  fvec4 acc[16][2];  // [xi][ci half]
-#pragma unroll
-  for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) acc[xi][h] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 1
-  for (int e = 0; e < 8; ++e) {  // eighths of the 64 output channels of conv2
-    const int q = e >> 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's DMAs of eighth e (and quarter q) landed
-    __syncthreads();  // everyone's landed, and every wave is done with the buffers refilled next
-    if (e + 1 < 8) dma_ur(e + 1, (e + 1) & 1);
-    if (!(e & 1) && q + 1 < 4) dma_pairs(q + 1, (q + 1) & 1);
-    if (!active) continue;
-    const fvec4* ub = reinterpret_cast<const fvec4*>(lds + ((e & 1) ? BD_UR1 : BD_UR0));
-    const float* pv = lds + ((q & 1) ? BD_PV1 : BD_PV0);
-    const uint8_t* pc = reinterpret_cast<const uint8_t*>(lds + ((q & 1) ? BD_PC1 : BD_PC0));
-    float pn[16];  // the k-step's 4x4 patch, [row][col]
-    auto load_patch = [&](int st) {  // k-step st of the eighth: channel 8 (e & 1) + 4 st + kq of the quarter
-      const int ch = 8 * (e & 1) + 4 * st + kq;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float dv = pv[woff[a][b] + ch];
-          const uint32_t c = pc[woff[a][b] + ch];
-          const float v = (wval[a][b] && (c & 0x80)) ? dv : 0.0f;
-          const int sel = c & 3;
-          pn[4 * (2 * a) + 2 * b] = sel == 0 ? v : 0.0f;
-          pn[4 * (2 * a) + 2 * b + 1] = sel == 1 ? v : 0.0f;
-          pn[4 * (2 * a + 1) + 2 * b] = sel == 2 ? v : 0.0f;
-          pn[4 * (2 * a + 1) + 2 * b + 1] = sel == 3 ? v : 0.0f;
-        }
-    };
-    auto v_row = [&](int i, float (&v)[16]) {
-      float t[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float d_0 = pn[c], d_1 = pn[4 + c], d_2 = pn[8 + c], d_3 = pn[12 + c];
-        t[c] = (i == 0) ? d_0 - d_2 : (i == 1) ? d_1 + d_2 : (i == 2) ? d_2 - d_1 : d_1 - d_3;
-      }
-      v[4 * i + 0] = t[0] - t[2];
-      v[4 * i + 1] = t[1] + t[2];
-      v[4 * i + 2] = t[2] - t[1];
-      v[4 * i + 3] = t[1] - t[3];
-    };
-    auto load_b = [&](int st, int m, fvec4 (&b)[2]) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) b[h] = ub[((4 * st + kq) * C1 + 16 * h + tl) * 4 + (m ^ swz)];
-    };
-    float vc[16], vn[16];
-    load_patch(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v_row(i, vc);
-    fvec4 bc[2], bn[2];
-    load_b(0, 0, bc);
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      if (st < 1) load_patch(st + 1);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        if (m < 3) load_b(st, m + 1, bn);
-        else if (st < 1) load_b(st + 1, 0, bn);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int xx = 0; xx < 4; ++xx) {
-          if (xx == (m == 0 ? 2 : 0)) {
-            if (m == 0) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(pn[k]));
-          }
-#pragma unroll
-          for (int h = 0; h < 2; ++h) acc[4 * m + xx][h] = mfma16(vc[4 * m + xx], bc[h][xx], acc[4 * m + xx][h]);
-        }
-        if (st < 1) v_row(m, vn);
-        __builtin_amdgcn_sched_barrier(0);
-        bc[0] = bn[0];
-        bc[1] = bn[1];
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) vc[i] = vn[i];
-    }
-  }
-  // ---- epilogue (wave-local), as conv_bwd_data_kernel.  Lane (tl, kq) holds M[xi][tile 4kq + rr][ci 16h + tl].
-  const float* img_s = lds + BD_IMG;
-  float w1b[3][2];
-#pragma unroll
-  for (int s3 = 0; s3 < 3; ++s3)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = 4 * s3 + kq, ci = 16 * h + tl;
-      w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
-    }
-  fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  fvec4 gacc1 = gacc;
-  if (active) {
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int tA = min(gt0 + 4 * (tl >> 2) + rr, BWD_TILES - 1);
-      const int pyA = 2 * (tA / 13) + ((tl & 3) >> 1), pxA = 2 * (tA % 13) + (tl & 1);
-      float a1v[3];
-#pragma unroll
-      for (int s3 = 0; s3 < 3; ++s3) {
-        const int k = 4 * s3 + kq;
-        a1v[s3] = (k < 9) ? img_s[(pyA + k / 3) * IMG + pxA + k % 3] : ((k == 9) ? 1.0f : 0.0f);
-      }
-      const int tB = gt0 + 4 * kq + rr;
-      const bool valid = tB < BWD_TILES && tB < tile0 + BWD_BAND_TILES;
-      const int tBc = min(tB, BWD_TILES - 1);
-      fvec4 z[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        fvec4 c1 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) c1 = mfma16(a1v[s3], w1b[s3][h], c1);
-        float tv[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float m0 = acc[4 * i][h][rr], m1 = acc[4 * i + 1][h][rr], m2 = acc[4 * i + 2][h][rr],
-                      m3 = acc[4 * i + 3][h][rr];
-          tv[i][0] = (m0 + m1) + m2;
-          tv[i][1] = (m1 - m2) - m3;
-        }
-        float y[4];
-        y[0] = (tv[0][0] + tv[1][0]) + tv[2][0];
-        y[1] = (tv[0][1] + tv[1][1]) + tv[2][1];
-        y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
-        y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) z[h][qq] = (valid && c1[qq] > 0.0f) ? y[qq] : 0.0f;
-      }
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int py = 2 * (tBc / 13) + (qq >> 1), px = 2 * (tBc % 13) + (qq & 1);
-        const float pv = (tl < 9) ? img_s[(py + tl / 3) * IMG + px + tl % 3] : 0.0f;
-        const float av = (tl < 9) ? pv : ((tl == 9) ? 1.0f : 0.0f);
-        gacc = mfma16(av, z[0][qq], gacc);
-        gacc1 = mfma16(av, z[1][qq], gacc1);
-      }
-    }
-  }
-  float* red_s = lds + BD_RED;
-#pragma unroll
-  for (int reg = 0; reg < 4; ++reg) {
-    const int k = 4 * kq + reg;
-    if (k < 10) {
-      red_s[wave * 320 + k * 32 + tl] = gacc[reg];
-      red_s[wave * 320 + k * 32 + 16 + tl] = gacc1[reg];
-    }
-  }
-  __syncthreads();
-  float* out = w1_part + (((int64_t)r * bmax + j) * BWD_BANDS + band) * MPLC_CNN_W1P;
-  for (int e = tid; e < 10 * 32; e += BWD_THREADS)
-    out[e] = (red_s[e] + red_s[320 + e]) + (red_s[640 + e] + red_s[960 + e]);
-}
-
-// ------------------------------------------------------------------------------------------------
 // conv2 weight gradient in Winograd form F(3x3, 2x2): per 2x2 tile of dZ2 (= one pooling window) and the
 // 4x4 conv1 patch it sees,  dW2[3x3] += G^T [ (A delta A^T) (.) (B^T d B) ] G  (the transposed dual of the
 // forward's F(2x2, 3x3); A, B, G are the forward's matrices).  The sum over tiles runs in the transformed
@@ -1839,13 +1588,8 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   if (ph & MPLC_PHASE_BACK) {
   winograd_w2r_kernel<<<dim3(C1 * C2 / 256, R), 256, 0, s>>>(t->params, S, t->cnt, t->w2t);
   PROF_BEGIN(5);
-#ifdef MPLC_BWD_DMA
-  conv_bwd_data_dma_kernel<<<dim3(BWD_BANDS, B, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t,
-                                                                         t->dpooled, t->code, t->w1_part);
-#else
   conv_bwd_data_kernel<<<dim3(BWD_BANDS, (B + BWD_SPB - 1) / BWD_SPB, R), BWD_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->params, S, t->w2t, t->dpooled,
                                                           t->code, t->w1_part);
-#endif
   PROF_END(5);
   PROF_BEGIN(6);
   conv_wgrad_kernel<<<dim3(t->w2_splits, R), WG_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->w2_splits, t->params,
