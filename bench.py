@@ -771,6 +771,10 @@ def bench_cifar(args, rank, world, sub=False):
                                        for k in range(1, args.cifar_partners + 1)},
                    "train_samples_per_step_this_rank": int(samples / max(1, steps)),
                    "shapley_estimate": [round(float(v), 5) for v in c.contributivity_scores],
+                   # planning (mplc.mc.plan_frontier / adaptive waves): coalitions trained vs counted by the
+                   # estimator; the difference is speculation the sequential loop did not ask for
+                   "coalitions_trained": int(eng.stats.get("coalitions", 0) // max(1, steps + warm)),
+                   "frontier_plan": getattr(c, "plan_stats", None),
                    "replicas_per_launch": eng.stats.get("replicas", 0) / max(1, eng.stats.get("batches", 1)),
                    "lockstep_batches": eng.stats.get("batches", 0),
                    "test_eval_s": round(eng.stats.get("test_eval_s", 0.0), 2),
