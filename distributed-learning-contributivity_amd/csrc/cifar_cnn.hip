@@ -9,7 +9,8 @@
 //   dense5_fwd     d4 -> d5 = dropout(relu(d4 W5 + b5))                   A in LDS, W5 streamed
 //   head           Dense(10) + softmax-CE gradient, dW6 + RMSprop, dh5 = (dl W6^T) * dropout' * relu'
 //   dense5_bwd     per 16-row slice of W5: dd4 = dh5 W5^T, dW5 = d4^T dh5, RMSprop(W5) in one pass; the
-//                  epilogue routes dd4 through dropout' and the pool into the dense dz4 (relu' included)
+//                  epilogue routes dd4 through dropout' and the pool's mask into the pooled dz4 (the conv4
+//                  gradient kernels un-pool it, and conv3's data gradient writes dz2 pooled the same way)
 //   wino_u<1>      W2|W3|W4 -> the rotated, channel-swapped kernels in Winograd form for the data gradients
 //   conv4 wgrad/dgrad, conv3 wgrad/dgrad (epilogue: dropout' + un-pool into dz2), conv2 wgrad/dgrad,
 //   conv1 wgrad    data gradients are Winograd F(2x2,3x3) like the forward (full/same padding, rotated
@@ -465,6 +466,50 @@ __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Stage rows iy0 .. iy0 + NR - 1, columns ix0 .. ix0 + NC - 1 (iy0, ix0, NR, NC even: whole pooling windows) of a
+// dense gradient held POOLED [HP][WP][C] with its pool codes (argmax = code & 3; dropout' and the pool's positive
+// mask already applied by the producer) into an LDS image [NR][NC][CP floats], channels 0 .. C - 1: each window's
+// value at its argmax pixel, 0 at the other three and outside the pooled grid (an odd dense size's last row / column
+// belongs to no window).  Window-major: one (window, channel quad) per item, so one 16-B value load and one 4-B code
+// load feed 4 pixels.  The LDS image is exactly what the dense un-pooled tensor held.
+template <int HP, int WP, int C, int NR, int NC, int CP, int NTHR>
+__device__ __forceinline__ void stage_unpool(const float* __restrict__ pooled, const uint8_t* __restrict__ codes,
+                                             int iy0, int ix0, float* __restrict__ dst, int tid) {
+  constexpr int C4 = C / 4;
+  constexpr int TOT = (NR / 2) * (NC / 2) * C4;
+  constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+  fvec4 val[NIT];
+  uint32_t cw[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = tid + k * NTHR;
+    const int win = e / C4, c4 = e % C4;
+    const int py = iy0 / 2 + win / (NC / 2), px = ix0 / 2 + win % (NC / 2);
+    const bool ok = e < TOT && py >= 0 && py < HP && px >= 0 && px < WP;
+    const int pidx = (py * WP + px) * C + 4 * c4;
+    const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? pooled + pidx : pooled);
+    const uint32_t c = *reinterpret_cast<const uint32_t*>(ok ? codes + pidx : codes);
+    val[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    cw[k] = c;
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int e = tid + k * NTHR;
+    if (e < TOT) {
+      const int win = e / C4, c4 = e % C4;
+      float* d0 = dst + ((2 * (win / (NC / 2))) * NC + 2 * (win % (NC / 2))) * CP + 4 * c4;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float* d = d0 + ((p >> 1) * NC + (p & 1)) * CP;
+        d[0] = (cw[k] & 3) == (uint32_t)p ? val[k].x : 0.0f;
+        d[1] = ((cw[k] >> 8) & 3) == (uint32_t)p ? val[k].y : 0.0f;
+        d[2] = ((cw[k] >> 16) & 3) == (uint32_t)p ? val[k].z : 0.0f;
+        d[3] = ((cw[k] >> 24) & 3) == (uint32_t)p ? val[k].w : 0.0f;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) {  // o = G g (one column)
   o[0] = g[0];
   o[1] = 0.5f * ((g[0] + g[1]) + g[2]);
@@ -587,7 +632,7 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
-template <int HI, int WI, int CI, int CO, int PAD, int BTY, int EPI>
+template <int HI, int WI, int CI, int CO, int PAD, int BTY, int EPI, int UPI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_kernel(const ConvArgs a) {
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
@@ -618,7 +663,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int ty0 = band * BTY;
   const int bty = min(BTY, TYT - ty0);  // tile rows of this band
   const int ntile = bty * TXT;
-  {  // stage input rows 2 ty0 - PAD .. + LR, columns -PAD .. + LC (zero outside the input)
+  if constexpr (UPI) {  // the input is a POOLED gradient [HI/2][WI/2][CI] with its pool codes: un-pooled here
+    static_assert(PAD % 2 == 0 && LR % 2 == 0 && LC % 2 == 0, "the staged region must be whole pooling windows");
+    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, 256>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
+                                                       2 * ty0 - PAD, -PAD, in_s, tid);
+  } else {  // stage input rows 2 ty0 - PAD .. + LR, columns -PAD .. + LC (zero outside the input)
     constexpr int C4 = CI / 4;
     constexpr int TOT = LR * LC * C4;
     constexpr int NIT = (TOT + 255) / 256;
@@ -782,14 +831,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 o[o_i] = fmaxf(y[q] + bias[co], 0.0f);
               } else if constexpr (EPI == EPI_BWD_MASK) {
                 o[o_i] = act[o_i] > 0.0f ? y[q] : 0.0f;
-              } else {  // dropout' + un-pool into the dense dZ (2HO x 2WO) of the layer below
+              } else {  // dropout' + the pool's positive mask: the POOLED gradient of the layer below, whose
+                        // argmax (code & 3) the consumers un-pool on the fly (a quarter of the dense dZ's bytes)
                 const uint32_t c = cd[o_i];
                 const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
-                const bool pos = (c & CODE_POS) != 0;
-                const int sel = c & 3;
-#pragma unroll
-                for (int p4 = 0; p4 < 4; ++p4)
-                  o[((2 * yy + (p4 >> 1)) * (2 * WO) + 2 * xx + (p4 & 1)) * CO + co] = (pos && sel == p4) ? dv : 0.0f;
+                o[o_i] = (c & CODE_POS) ? dv : 0.0f;
               }
             }
           }
@@ -820,6 +866,7 @@ struct WgArgs {
   const float* dz;
   float* wpart;
   int off_w, off_b;
+  const uint8_t* dz_code;  // UPZ (wino_wgrad_kernel): dz is the POOLED gradient, un-pooled with these argmax codes
 };
 
 template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BR, int NW, int WPE = 0>
@@ -1005,7 +1052,7 @@ void wgrad_kernel(const WgArgs a) {
 // half the LDS reads and 2/3 of the VALU per MFMA of the row-per-wave form at CO = 32 (which issues 8 MFMAs
 // per 8 reads and 12 adds).  NW waves per block = the band's 16-tile groups.
 // ------------------------------------------------------------------------------------------------
-template <int HI, int WI, int CI, int CO, int PAD, int BTY, int NW, int EPI>
+template <int HI, int WI, int CI, int CO, int PAD, int BTY, int NW, int EPI, int UPI = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wl_kernel(const ConvArgs a) {
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
@@ -1030,7 +1077,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int ty0 = band * BTY;
   const int bty = min(BTY, TYT - ty0);
   const int ntile = bty * TXT;
-  {
+  if constexpr (UPI) {  // the input is a POOLED gradient [HI/2][WI/2][CI] with its pool codes: un-pooled here
+    static_assert(PAD % 2 == 0 && LR % 2 == 0 && LC % 2 == 0, "the staged region must be whole pooling windows");
+    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, NTHR>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
+                                                        2 * ty0 - PAD, -PAD, in_s, tid);
+  } else {
     constexpr int C4 = CI / 4;
     constexpr int TOT = LR * LC * C4;
     constexpr int NIT = (TOT + NTHR - 1) / NTHR;
@@ -1208,7 +1259,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // fold their row of the inverse transform (P_i = M_i G) and exchange it through LDS, 16 input channels at a
 // time.  Samples, bands and tiles in a fixed order: sums independent of which replicas share the launch.
 // ------------------------------------------------------------------------------------------------
-template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BTY, int CIB>
+template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BTY, int CIB, int UPZ = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wgrad_kernel(const WgArgs a) {
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr int TY = (HOV + 1) / 2, TX = (WOV + 1) / 2;
@@ -1285,7 +1336,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
       }
-      {  // dZ rows 2 ty0 .. (zero beyond HOV x WOV); db from the same loads (chunk 0 only)
+      if constexpr (UPZ) {  // pooled dZ [HO/2][WO/2][CO] with its codes, un-pooled window-major; db below
+        static_assert(ZR % 2 == 0 && ZC % 2 == 0 && HOV == 2 * (HO / 2) && WOV == 2 * (WO / 2), "whole windows");
+        stage_unpool<HO / 2, WO / 2, CO, ZR, ZC, COP, 256>(Z, a.dz_code + slot * ((HO / 2) * (WO / 2) * CO), 2 * ty0,
+                                                           0, z_s, tid);
+      } else {  // dZ rows 2 ty0 .. (zero beyond HOV x WOV); db from the same loads (chunk 0 only)
         constexpr int Z4 = CO / 4;
         constexpr int TOT = ZR * ZC * Z4;
         constexpr int NIT = (TOT + 255) / 256;
@@ -1314,6 +1369,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
       __syncthreads();
+      if constexpr (UPZ) {  // db from the staged image, summed in the dense staging's order (bit-identical)
+        if (chn == 0) {
+          constexpr int Z4 = CO / 4;
+          constexpr int TOT = ZR * ZC * Z4;
+          static_assert(256 % Z4 == 0, "db needs a fixed channel quad per thread");
+#pragma unroll
+          for (int k = 0; k < (TOT + 255) / 256; ++k) {
+            const int e4 = tid + k * 256;
+            if (e4 < TOT) {
+              const float* d = z_s + (e4 / Z4) * COP + 4 * (e4 % Z4);
+              gb += fvec4{d[0], d[1], d[2], d[3]};
+            }
+          }
+        }
+      }
       const int ntile = bty * TX;
 #pragma unroll 1
       for (int t0 = 0; t0 < ntile; t0 += 4) {
@@ -1621,7 +1691,8 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 // each: every access instruction covers 512 contiguous bytes of a row); dh5 is staged in LDS once per
 // block for its 4 row groups:
 //   dd4[j][k] = sum_n dh5[j][n] W5[k][n];  dW5[k][n] = sum_j d4[j][k] dh5[j][n];  db5 (slice-0 block).
-// dd4 goes through dropout'(.25) and the 2x2 pool (argmax + relu' from code4) into the dense dz4.
+// dd4 goes through dropout'(.25) and the pool's positive mask into the POOLED dz4 [6][6][64] (conv4's gradient
+// kernels un-pool it with code4's argmax while staging).
 // HBM-bound: W5 and its accumulator are read and written once per step (the accumulator is not read on a
 // fresh optimizer's first step).
 // ------------------------------------------------------------------------------------------------
@@ -1702,10 +1773,7 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
         avn[i] = cfg.reset ? z4 : __builtin_nontemporal_load(Ran + 32 * i);
       }
     }
-    const int k = kb + grp * D5_ROWS + rowl;
-    const int pix = k / 64, ch = k % 64;
-    const int py = pix / 6, px = pix % 6;
-    const int dzoff = ((2 * py + (c32 >> 1)) * 13 + 2 * px + (c32 & 1)) * 64 + ch;
+    const int k = kb + grp * D5_ROWS + rowl;  // the d4 element (flatten order: pooled row, column, channel)
     fvec4 g[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) g[i] = z4;
@@ -1730,11 +1798,10 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
         d += dpp_partner<DPP_HALF_MIRROR>(d);
         d += dpp_partner<DPP_MIRROR>(d);
         d += __shfl_xor(d, 16, 64);
-        if (c32 < 4) {  // un-pool: lane c32 = q writes window pixel q
+        if (c32 == 0) {  // dropout' and the pool's positive mask: the POOLED dz4 (conv4's gradients un-pool it)
           const uint32_t c = c_s[jj * KB + grp * D5_ROWS + rowl];
           const float v = (c & CODE_KEEP) ? d * SCALE_25 : 0.0f;
-          const bool hit = (c & CODE_POS) && (int)(c & 3) == c32;
-          dZ4[((int64_t)r * bmax + c0 + jj) * MPLC_CIFAR_DZ4 + dzoff] = hit ? v : 0.0f;
+          dZ4[((int64_t)r * bmax + c0 + jj) * MPLC_CIFAR_DZ4 + k] = (c & CODE_POS) ? v : 0.0f;
         }
       }
     }
@@ -1833,16 +1900,19 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 // conv3's data gradient keeps the row form: its bands hold 2 tile groups, and the wave-local form with 2-wave
 // blocks measured slower (4585 vs 4264 ms over a config #4 run, profiles/r03_driver_bench_v2.json)
 #define CONV3_DGRAD wino_kernel<15, 15, 64, 32, 1, 4, EPI_BWD_UNPOOL>        /* 8x8 tiles, 2 bands, 63.7 KB */
-#define CONV2_DGRAD wino_wl_kernel<30, 30, 32, 32, 2, 4, 4, EPI_BWD_MASK>    /* 64 tiles, 4 bands, 44.9 KB */
+// conv2's data / weight gradients read dZ2 POOLED (conv3's data gradient writes [15][15][32] + the pool codes) and
+// un-pool it while staging: a quarter of the dense gradient's HBM bytes
+#define CONV2_DGRAD wino_wl_kernel<30, 30, 32, 32, 2, 4, 4, EPI_BWD_MASK, 1> /* 64 tiles, 4 bands, 44.9 KB */
 #define CONV3_DGRAD_NT 256
 #define CONV3_FWD wino_kernel<15, 15, 32, 64, 1, 8, EPI_FWD>          /* 8x8 tiles,    1 band,  59.7 KB */
 #define CONV4_FWD wino_kernel<15, 15, 64, 64, 0, 6, EPI_FWD_POOL>     /* 6x6 windows,  1 band,  67.9 KB */
-#define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK>   /* 8x8 tiles,    2 bands, 63.7 KB */
+// conv4's gradients read dz4 POOLED ([6][6][64] + code4, written by dense5_bwd) and un-pool it while staging
+#define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK, 1>   /* 8x8 tiles,    2 bands, 63.7 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 // Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
-#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32>  /* 15x15 tiles, 5 bands, 56.9 KB */
+#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1>  /* 15x15 tiles, 5 bands, 56.9 KB */
 #define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 57.1 KB */
-#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32>  /* 6x6 tiles, 1 band, 2 ci chunks */
+#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1>  /* 6x6 tiles, 1 band, 2 ci chunks */
 
 inline int launch_status() {
   const hipError_t e = hipGetLastError();
@@ -1995,11 +2065,12 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   // the data gradients' kernels (rotated, channels swapped) in Winograd form, over the forward's
   wino_u_kernel<1><<<dim3(7168 / 256, R), 256, 0, s>>>(t->params, STRIDE, t->cnt, t->wt);
   const int SP = t->wg_splits;
-  WgArgs w4{t->a3, 0, t->idx, t->cnt, B, SP, t->dz4, t->wpart, (int)OFF_W4, (int)OFF_B4};
+  WgArgs w4{t->a3, 0, t->idx, t->cnt, B, SP, t->dz4, t->wpart, (int)OFF_W4, (int)OFF_B4, t->code4};  // dz4 pooled
   PROF_BEGIN(8);
   CONV4_WGRAD<<<dim3(SP, R, 2), 256, 0, s>>>(w4);
   PROF_END(8);
   ConvArgs g4 = conv_args(t->dz4, 0, 0, nullptr, t->cnt, 0, B, t->wt + WU_4, MPLC_CIFAR_WT);
+  g4.code_in = t->code4;  // dz4 is pooled: un-pooled while staging
   g4.aux = t->a3;
   g4.out = t->dz3;
   PROF_BEGIN(9);
@@ -2015,12 +2086,13 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   PROF_BEGIN(11);
   CONV3_DGRAD<<<dim3(2, B, R), CONV3_DGRAD_NT, 0, s>>>(g3);
   PROF_END(11);
-  WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2};
+  WgArgs w2{t->a1, 0, t->idx, t->cnt, B, SP, t->dz2, t->wpart, (int)OFF_W2, (int)OFF_B2, t->code2};  // dz2 pooled
   PROF_BEGIN(12);
   CONV2_WGRAD<<<dim3(SP, R, 1), 256, 0, s>>>(w2);
   PROF_END(12);
   ConvArgs g2 = conv_args(t->dz2, 0, 0, nullptr, t->cnt, 0, B, t->wt + WU_2, MPLC_CIFAR_WT);
   g2.aux = t->a1;
+  g2.code_in = t->code2;  // dz2 is pooled: un-pooled while staging
   g2.out = t->dz1;
   PROF_BEGIN(13);
   CONV2_DGRAD<<<dim3(4, B, R), 256, 0, s>>>(g2);
