@@ -775,6 +775,7 @@ def bench_cifar(args, rank, world, sub=False):
                    # estimator; the difference is speculation the sequential loop did not ask for
                    "coalitions_trained": int(eng.stats.get("coalitions", 0) // max(1, steps + warm)),
                    "frontier_plan": getattr(c, "plan_stats", None),
+                   "sampling_iterations": getattr(c, "sampling_iterations", None),  # SMCS / WR_SMC to the stop rule
                    "replicas_per_launch": eng.stats.get("replicas", 0) / max(1, eng.stats.get("batches", 1)),
                    "lockstep_batches": eng.stats.get("batches", 0),
                    "test_eval_s": round(eng.stats.get("test_eval_s", 0.0), 2),

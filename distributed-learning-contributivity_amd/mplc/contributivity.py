@@ -784,6 +784,7 @@ class Contributivity:
                         keep_going[k][strata] = False
                 var[k] /= N ** 2
             v_max = np.max(var)
+        self.sampling_iterations = t  # the loop's iterations to its stopping rule (bench report)
         self._finish("Stratified MC Shapley", shap, np.sqrt(var))
 
     @staticmethod
@@ -901,6 +902,7 @@ class Contributivity:
                         keep_going[k][strata] = False
                 var[k] /= N ** 2
             v_max = np.max(var)
+        self.sampling_iterations = t  # the loop's iterations to its stopping rule (bench report)
         self._finish("WR_SMC Shapley", shap, np.sqrt(var))
 
     # --------------------------------------------------------------------------------------------

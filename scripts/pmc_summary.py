@@ -28,10 +28,14 @@ for k, v in tot.items():
           f"{2 * v['FETCH_SIZE'] / 1024 / 1024:9.2f}")
 
 # extra view: where the waves spend their cycles (SQ_WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY)
-print(f"\n{'kernel':44s} {'waves':>8s} {'wait_any':>8s} {'wait_ins':>8s} {'active':>8s} {'lds/mfma':>8s} {'ldswait':>8s}")
+print(f"\n{'kernel':44s} {'waves':>8s} {'wait_any':>8s} {'wait_ins':>8s} {'active':>8s} {'lds/mfma':>8s} {'ldswait':>8s} "
+      f"{'valu_use':>8s}")
 for k, v in tot.items():
     wc = v["SQ_WAVE_CYCLES"] + 1e-9
     mf = v["SQ_INSTS_MFMA"] + 1e-9
     print(f"{k[:44]:44s} {v['SQ_WAVES']:8.0f} {v['SQ_WAIT_ANY'] / wc:8.3f} {v['SQ_WAIT_INST_ANY'] / wc:8.3f} "
           f"{v['SQ_ACTIVE_INST_ANY'] / wc:8.3f} {(v['SQ_INSTS_LDS'] / mf if v['SQ_INSTS_MFMA'] > 0 else float('nan')):8.2f} "
-          f"{v['SQ_WAIT_INST_LDS'] / wc:8.3f}")
+          f"{v['SQ_WAIT_INST_LDS'] / wc:8.3f} "
+          # VALU pipe use: 4 cycles per wave64 VALU instruction over all SIMDs' cycles (an estimate: packed and
+          # transcendental ops differ)
+          f"{4 * v['SQ_INSTS_VALU'] / max(1.0, v['GRBM_GUI_ACTIVE'] / 8 * 1024):8.3f}")
