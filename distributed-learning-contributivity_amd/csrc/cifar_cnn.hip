@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "keyed.h"
+#include "xcd.h"
 #include "mplc_hip.h"
 #include "mplc_hip_cifar.h"
 
@@ -632,6 +633,9 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
+#ifndef MPLC_ROW_EPI_STAGE
+#define MPLC_ROW_EPI_STAGE 1  // wino_kernel: the data gradients' epilogue operand staged as bytes in LDS up front
+#endif
 template <int HI, int WI, int CI, int CO, int PAD, int BTY, int EPI, int UPI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_kernel(const ConvArgs a) {
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
@@ -651,9 +655,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int NK = CI / 4;
   static_assert(CI % 4 == 0 && CO % 32 == 0, "channel counts");
   static_assert((16 * CH) % 256 == 0, "output items per thread");
+  // the data gradients' epilogue operand (EPI_BWD_MASK: the ReLU' mask a > 0; EPI_BWD_UNPOOL: the pool codes) for
+  // the band's 2 BTY output rows, staged as bytes with the input band: its global loads share the staging's latency
+  // instead of stalling the output phase of every group
+  constexpr bool STAGE_EPI = MPLC_ROW_EPI_STAGE && (EPI == EPI_BWD_MASK || EPI == EPI_BWD_UNPOOL);
+  constexpr int ER = 2 * BTY;
   __shared__ float in_s[LR * ROWP];
   __shared__ float t_s[8 * TQ];
-  const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+  __shared__ uint32_t e_s[STAGE_EPI ? ER * WO * CO / 4 : 1];
+  const LogicalBlock lbk = xcd_block3();  // (band, sample, replica): a replica's blocks share one XCD's L2 (its U)
+  const int band = lbk.x, j = lbk.y, r = lbk.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
   if (j >= count) return;
   const int tid = threadIdx.x;
@@ -691,6 +702,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         d[1] = v[k].y;
         d[2] = v[k].z;
         d[3] = v[k].w;
+      }
+    }
+  }
+  if constexpr (STAGE_EPI) {
+    constexpr int TOT = ER * WO * (CO / 4);
+    constexpr int NIT = (TOT + 255) / 256;
+    const float* ax = a.aux + slot * (HO * WO * CO);
+    const uint8_t* cx = a.code_in + slot * (HO * WO * CO);
+    uint32_t ev[NIT];
+    fvec4 fv[EPI == EPI_BWD_MASK ? NIT : 1];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + 256 * k;
+      const int px = e / (CO / 4), c4 = e % (CO / 4);
+      const int yy = 2 * ty0 + px / WO, xx = px % WO;
+      const bool ok = e < TOT && yy < HO;
+      const int64_t off = ok ? (int64_t)(yy * WO + xx) * CO + 4 * c4 : 0;
+      if constexpr (EPI == EPI_BWD_MASK) {
+        const fvec4 t = *reinterpret_cast<const fvec4*>(ax + off);
+        fv[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+      } else {
+        const uint32_t t = *reinterpret_cast<const uint32_t*>(cx + off);
+        ev[k] = ok ? t : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + 256 * k;
+      if (e < TOT) {
+        if constexpr (EPI == EPI_BWD_MASK)
+          ev[k] = (fv[k].x > 0.0f ? 1u : 0u) | (fv[k].y > 0.0f ? 0x100u : 0u) | (fv[k].z > 0.0f ? 0x10000u : 0u) |
+                  (fv[k].w > 0.0f ? 0x1000000u : 0u);
+        e_s[e] = ev[k];
       }
     }
   }
@@ -830,10 +874,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               if constexpr (EPI == EPI_FWD) {
                 o[o_i] = fmaxf(y[q] + bias[co], 0.0f);
               } else if constexpr (EPI == EPI_BWD_MASK) {
-                o[o_i] = act[o_i] > 0.0f ? y[q] : 0.0f;
+                if constexpr (STAGE_EPI) {
+                  o[o_i] = reinterpret_cast<const uint8_t*>(e_s)[((yy - 2 * ty0) * WO + xx) * CO + co] ? y[q] : 0.0f;
+                } else {
+                  o[o_i] = act[o_i] > 0.0f ? y[q] : 0.0f;
+                }
               } else {  // dropout' + the pool's positive mask: the POOLED gradient of the layer below, whose
                         // argmax (code & 3) the consumers un-pool on the fly (a quarter of the dense dZ's bytes)
-                const uint32_t c = cd[o_i];
+                const uint32_t c =
+                    STAGE_EPI ? reinterpret_cast<const uint8_t*>(e_s)[((yy - 2 * ty0) * WO + xx) * CO + co] : cd[o_i];
                 const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
                 o[o_i] = (c & CODE_POS) ? dv : 0.0f;
               }
@@ -1052,6 +1101,9 @@ void wgrad_kernel(const WgArgs a) {
 // half the LDS reads and 2/3 of the VALU per MFMA of the row-per-wave form at CO = 32 (which issues 8 MFMAs
 // per 8 reads and 12 adds).  NW waves per block = the band's 16-tile groups.
 // ------------------------------------------------------------------------------------------------
+#ifndef MPLC_WL_PRE_RR
+#define MPLC_WL_PRE_RR 4  // tile rows of the ReLU' operand loaded during the last k-step (0..4)
+#endif
 template <int HI, int WI, int CI, int CO, int PAD, int BTY, int NW, int EPI, int UPI = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wl_kernel(const ConvArgs a) {
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
@@ -1067,6 +1119,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   static_assert(CO == 32 && CI % 8 == 0, "wave-local form: 32 output channels");
   static_assert(NW * 16 >= BTY * TXT, "one 16-tile group per wave");
   __shared__ float in_s[LR * ROWP];
+  // (plain block order: the XCD-aware order measured +1-2 % on these wave-local kernels, scripts/r04/gpu_wlpm_es.sh)
   const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
   if (j >= count) return;
@@ -1167,14 +1220,45 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       }
     }
   };
+  // EPI_BWD_MASK: the epilogue's ReLU' operand (the layer input a, 8 values per tile row and lane) is loaded during
+  // the last k-step, so that its latency is covered by that k-step's 32 MFMAs (all 4 rows: conv2's data gradient
+  // -40 %, 2 registers spilled; 2 rows -25 %, 1 row -13 %; the peeled loop alone -4 %; bit-identical)
+  constexpr bool PRE_MASK = (EPI == EPI_BWD_MASK);
+  constexpr int PRE_RR = MPLC_WL_PRE_RR;
+  float mk[PRE_MASK && PRE_RR > 0 ? 8 * PRE_RR : 1];
+  auto load_mask = [&]() {
+    const float* ax = a.aux + slot * (HO * WO * CO);
+#pragma unroll
+    for (int rr = 0; rr < PRE_RR; ++rr) {
+      const int tt = min(16 * wave + 4 * kq + rr, ntile - 1);
+      const int ty = ty0 + tt / TXT, tx2 = tt % TXT;
+#pragma unroll
+      for (int cg = 0; cg < 2; ++cg)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int yy = min(2 * ty + (q >> 1), HO - 1), xx = min(2 * tx2 + (q & 1), WO - 1);
+          mk[(rr * 2 + cg) * 4 + q] = ax[(yy * WO + xx) * CO + 16 * cg + tl];
+        }
+    }
+  };
   float b0[32], b1[32];
   load_b(0, b0);
+  static_assert(NK % 2 == 0 && NK >= 2, "k-steps in pairs");
 #pragma unroll 1
-  for (int st = 0; st < NK; st += 2) {
+  for (int st = 0; st < NK - 2; st += 2) {
     load_b(st + 1, b1);
     kstep(st, b0);
-    if (st + 2 < NK) load_b(st + 2, b0);
+    load_b(st + 2, b0);
     kstep(st + 1, b1);
+  }
+  // the last pair peeled: b0 is dead after k-step NK - 2, its registers take the mask operand
+  load_b(NK - 1, b1);
+  kstep(NK - 2, b0);
+  if constexpr (PRE_MASK) load_mask();
+  kstep(NK - 1, b1);
+  if constexpr (PRE_MASK) {  // the loads stay ahead of the last k-step (not sunk to their use)
+#pragma unroll
+    for (int i = 0; i < 8 * PRE_RR; ++i) asm volatile("" : "+v"(mk[i]));
   }
   // output transform in registers: lane holds M[xi][tile 4 kq + rr][co 16 cg + tl]
   float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
@@ -1226,7 +1310,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           if (yy >= HO || xx >= WO) continue;
           const int o_i = (yy * WO + xx) * CO + co;
           if constexpr (EPI == EPI_BWD_MASK) {
-            o[o_i] = a.aux[slot * (HO * WO * CO) + o_i] > 0.0f ? y[q] : 0.0f;
+            const float av = rr < PRE_RR ? mk[((rr < PRE_RR ? rr : 0) * 2 + cg) * 4 + q]
+                                         : a.aux[slot * (HO * WO * CO) + o_i];
+            o[o_i] = av > 0.0f ? y[q] : 0.0f;
           } else if constexpr (EPI == EPI_BWD_UNPOOL) {
             const uint32_t c = a.code_in[slot * (HO * WO * CO) + o_i];
             const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
@@ -1500,13 +1586,14 @@ __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict
                                                          const uint64_t* __restrict__ drop_key,
                                                          float* __restrict__ H, uint8_t* __restrict__ code) {
   __shared__ float a_s[32 * (DF_K + 1)];
-  const int r = blockIdx.z;
-  const int m0 = blockIdx.x * 32;
+  const LogicalBlock lbk = xcd_block3();  // (sample tile, column slice, replica): a replica's W5 in one XCD's L2
+  const int r = lbk.z;
+  const int m0 = lbk.x * 32;
   const int count = cnt ? cnt[r] : cnt_all;
   if (m0 >= count) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.y * 128 + wave * 32;
+  const int n0 = lbk.y * 128 + wave * 32;
   const int kh = lane >> 5;
   const float* Ar = A + (int64_t)r * bmax * FEAT;
   const int gsrc = w5src ? w5src[r] : -1;  // W5 of a round's first step: the coalition row (not broadcast)
@@ -1715,8 +1802,9 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
   __shared__ fvec4 dh_s[D5_SCHUNK * (HID / 4)];
   __shared__ float p_s[D5_SCHUNK * KB];
   __shared__ uint8_t c_s[D5_SCHUNK * KB];
-  const int r = blockIdx.y;
-  const int kb = blockIdx.x * KB;
+  const LogicalBlock lbk = xcd_block3();  // (row slice, replica): a replica's dh5 rows in one XCD's L2
+  const int r = lbk.y;
+  const int kb = lbk.x * KB;
   const int count = cnt[r];
   if (count == 0) return;
   const int tid = threadIdx.x;
@@ -1826,7 +1914,7 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
       av[i] = avn[i];
     }
   }
-  if (blockIdx.x == 0) {
+  if (lbk.x == 0) {
     const float* dHs = dH + (int64_t)r * bmax * HID;
     for (int c = tid; c < HID; c += 256) {
       float gb = 0.0f;

@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include "mplc_hip.h"
 #include "keyed.h"
+#include "xcd.h"
 
 // Timing-experiment switches compile parts of a kernel out and give WRONG results by design (A/B probes of
 // where a kernel's time goes).  A product build must never carry one.
@@ -106,18 +107,6 @@ __device__ __forceinline__ floatx16 conv1_mfma(const float* img_s, int pix, int 
   const float a8 = img_s[pix + 2 * IMG + 2];
   acc = mfma32(kh ? 1.0f : a8, w1r[4], acc);
   return acc;
-}
-
-// XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs (block b and b + 8 share one,
-// MI355X_MICROARCH.md), so a replica's consecutive blocks would land on all 8 XCDs and each XCD's L2 would
-// fetch that replica's weights.  The flat block id is remapped so that each XCD walks a contiguous range of
-// logical blocks (replica-major): the blocks of one replica share an XCD and its L2.  The mapping only
-// permutes which workgroup does which tile of work; every result is bit-identical.
-__device__ __forceinline__ int64_t xcd_block() {
-  const int64_t n = (int64_t)gridDim.x * gridDim.y * gridDim.z;
-  const int64_t b = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
-  const int64_t q = n / 8;
-  return b < 8 * q ? (b % 8) * q + b / 8 : b;
 }
 
 // accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
@@ -889,6 +878,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   __shared__ fvec4 ur_s[BWD_UQ / 4];
   __shared__ float img_s[IMG * IMG];
   __shared__ float red_s[4][10 * 32];
+  __shared__ float w1_s[10 * C1];  // conv1's taps and bias (the epilogue's B operand), staged up front
   const int64_t lb = xcd_block();  // logical block (band, sample group, r), replica-major
   const int band = (int)(lb % BWD_BANDS);
   const int jg = (int)((lb / BWD_BANDS) % gridDim.y);
@@ -933,6 +923,9 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   };
   fetch(j_begin, 0);
   load_img(j_begin);
+  // conv1's weights for the epilogue: read here, where their latency hides behind the first quarter's staging,
+  // instead of from global memory at the epilogue's start (one exposed load round trip per block)
+  for (int e = tid; e < 10 * C1; e += BWD_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
   {
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
@@ -1080,7 +1073,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = 4 * s3 + kq, ci = 16 * h + tl;
-      w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
+      w1b[s3][h] = (k < 10) ? w1_s[k * C1 + ci] : 0.0f;
     }
   fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
   fvec4 gacc1 = gacc;
@@ -1197,6 +1190,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   __shared__ float smem[(WG_A1 + 24 * WG_VS * 2 > 4 * WG_PX) ? WG_A1 + 24 * WG_VS * 2 : 4 * WG_PX];
   __shared__ float img_s[IMG * IMG];
   __shared__ float gb_s[4][C2];
+  __shared__ float w1_s[10 * C1];      // conv1's taps and bias for the 16x16x4 recompute pieces (read every band)
   float* const a1_s = smem;            // [6][26][WG_CS]
   int2* const vq_s = reinterpret_cast<int2*>(smem + WG_A1);  // [24 windows][WG_VS]: (value bits, argmax)
   const int sp = blockIdx.x;
@@ -1214,6 +1208,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const float* P = params + (int64_t)r * stride;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
+  for (int e = tid; e < 10 * C1; e += WG_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
   float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread stages has that channel)
   float pdv[WG_PRE];
   uint32_t pcd[WG_PRE];
@@ -1296,7 +1291,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int s3 = 0; s3 < 3; ++s3) {
           const int k = 4 * s3 + kq;
           const float av = (k < 9) ? img_s[(4 * band + p / A1 + k / 3) * IMG + p % A1 + k % 3] : ((k == 9) ? 1.0f : 0.0f);
-          const float wv = (k < 9) ? P[OFF_W1 + k * C1 + 16 * h + tl] : ((k == 9) ? P[OFF_B1 + 16 * h + tl] : 0.0f);
+          const float wv = (k < 10) ? w1_s[k * C1 + 16 * h + tl] : 0.0f;
           c1 = mfma16(av, wv, c1);
         }
 #pragma unroll

@@ -447,23 +447,32 @@ class TrainBatch:
             first.append(acc)
         else:
             first = self.coal_first
-        args = []
+        # every run's offsets, weights and scales go to the device in one copy per dtype (views per run): an early-
+        # stopping epoch end rebuilds the runs, and per-run copies stalled the stream for tens of microseconds each
+        f_all, f64_all, spans = [], [], []
         for run in runs:
-            f = torch.tensor([first[ci] - first[run[0]] for ci in run] + [first[run[-1] + 1] - first[run[0]]],
-                             **self.i32)
+            f = [first[ci] - first[run[0]] for ci in run] + [first[run[-1] + 1] - first[run[0]]]
             w, sc = [], []
             for ci in run:
                 ww, scl = aggregation_weights([sizes[p] for p in self.coalitions[ci]], self.eng.aggregation)
                 w.extend(ww)
                 sc.append(scl)
+            spans.append((len(f_all), len(f), len(f64_all), len(w), len(sc)))
+            f_all.extend(f)
+            f64_all.extend(w)
+            f64_all.extend(sc)
+        f_dev = torch.tensor(f_all, **self.i32) if f_all else None
+        x_dev = torch.tensor(f64_all, dtype=torch.float64, device=self.dev) if f64_all else None
+        args = []
+        for run, (fo, fn, xo, wn, sn) in zip(runs, spans):
             # the broadcast may skip W3 / W5 only if every member trains in every round: a round's first step
             # is what reloads them from the coalition row, and a partner with an empty minibatch (fewer rows
             # than minibatch_count) has no step in that round, yet enters the average with the round's global
             # model (the reference's fresh model from the global weights, mplc/multi_partner_learning.py:319)
             full_bcast = any(self.eng.bounds[p][m + 1] == self.eng.bounds[p][m]
                              for ci in run for p in self.coalitions[ci] for m in range(self.eng.minibatch_count))
-            args.append((self.coal_first[run[0]], run[0], len(run), f, torch.tensor(w, dtype=torch.float64, device=self.dev),
-                         torch.tensor(sc, dtype=torch.float64, device=self.dev), full_bcast))
+            args.append((self.coal_first[run[0]], run[0], len(run), f_dev[fo:fo + fn], x_dev[xo:xo + wn],
+                         x_dev[xo + wn:xo + wn + sn], full_bcast))
         return args
 
     def step(self, s):
@@ -513,10 +522,13 @@ class TrainBatch:
     def snap_row(self, ci):
         return sum(len(self.coalitions[c]) for c in range(ci) if not self.coal_is_single[c])
 
-    def stop(self, ci):
+    def stop(self, cis):
+        """Coalitions `cis` stop training (early stopping): their replicas go idle and the aggregation runs are
+        rebuilt once for all of them (one epoch end can stop hundreds of coalitions)."""
         import torch
-        self.stopped[ci] = True
-        self.kind_host[self.coal_first[ci]:self.coal_first[ci + 1]] = REP_IDLE
+        for ci in cis:
+            self.stopped[ci] = True
+            self.kind_host[self.coal_first[ci]:self.coal_first[ci + 1]] = REP_IDLE
         ra = self.rep_arr.copy()
         ra["kind"] = self.kind_host
         self.rep_t.copy_(torch.from_numpy(ra.view(np.uint8).copy()).to(self.dev))
@@ -632,16 +644,20 @@ class CnnBatchTrainer:
                 st.aggregate(epoch_end=(s + 1) % per_epoch_fed == 0)
                 if use_es and (s + 1) % per_epoch_fed == 0:
                     e = (s + 1) // per_epoch_fed - 1
+                    stops = []
                     for ci in fed:
                         h = val_hist[orig[ci]]
                         if not st.stopped[ci] and e >= PATIENCE and h[e] > h[e - PATIENCE]:
                             epochs_done[orig[ci]] = e + 1
-                            st.stop(ci)
+                            stops.append(ci)
+                    if stops:
+                        st.stop(stops)
             if use_es and spe:
                 # singleton epoch ends: Keras EarlyStopping(monitor='val_loss', patience=10, min_delta=0)
                 ends = [ci for ci in spe if not st.stopped[ci] and (s + 1) % spe[ci] == 0
                         and (s + 1) // spe[ci] <= epochs]
                 if ends:
+                    stops = []
                     for ci, l in zip(ends, self._val_loss(st.params, [st.coal_first[c] for c in ends])):
                         e = (s + 1) // spe[ci] - 1
                         o = orig[ci]
@@ -652,7 +668,9 @@ class CnnBatchTrainer:
                             es_wait[o] += 1
                             if es_wait[o] >= PATIENCE:
                                 epochs_done[o] = e + 1
-                                st.stop(ci)
+                                stops.append(ci)
+                    if stops:
+                        st.stop(stops)
             if st.stopped.all():
                 break
         if rec is not None:
