@@ -119,6 +119,9 @@ __device__ __forceinline__ RmsCfg rms_cfg(int t, float lr, float rho, float omr,
 }
 
 __device__ __forceinline__ void rms_apply(float& p, float& a, float g, const RmsCfg& c) {
+  // Keras evaluates rho a + (1 - rho) g^2 as separate multiplies and an add: no fused multiply-add here, in every
+  // kernel (the compiler's contraction otherwise depends on how it vectorised the caller)
+#pragma clang fp contract(off)
   const float a0 = c.reset ? 0.0f : a;
   const float an = c.rho * a0 + c.one_m_rho * (g * g);
   p = p - c.lr_t * g / (sqrtf(an) + c.eps);
@@ -1783,6 +1786,9 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 // HBM-bound: W5 and its accumulator are read and written once per step (the accumulator is not read on a
 // fresh optimizer's first step).
 // ------------------------------------------------------------------------------------------------
+#ifndef MPLC_D5_MFMA
+#define MPLC_D5_MFMA 1  // dense5_bwd_mfma_kernel (bit-identical MFMA form) instead of the VALU form
+#endif
 constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
 #ifndef MPLC_D5_GROUPS
 #define MPLC_D5_GROUPS 4
@@ -1913,6 +1919,185 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
       w[i] = wn[i];
       av[i] = avn[i];
     }
+  }
+  if (lbk.x == 0) {
+    const float* dHs = dH + (int64_t)r * bmax * HID;
+    for (int c = tid; c < HID; c += 256) {
+      float gb = 0.0f;
+      for (int jj = 0; jj < count; ++jj) gb += dHs[(int64_t)jj * HID + c];
+      const int64_t o = (int64_t)r * STRIDE + OFF_B5 + c;
+      rms_apply(params[o], rms[o], gb, cfg);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dense5_bwd with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense5_bwd_kernel (the matrix core
+// accumulates as the fmaf chain in k order, scripts/probes/mfma_order.hip; same reasoning as mnist_cnn.hip's
+// dense1_bwd_adam_mfma_kernel):
+//   dW5: the VALU chain over the samples in order -> MFMA K = 4 samples chained over sample quads;
+//   dd4: the VALU form's 32 partials (lane c32 of a row: columns 4 c32 + 128 i + q, i outer, q inner) -> per c32
+//        an MFMA chain over i with K = q, then the same 5-level tree over c32: levels 0-2 in registers (a wave owns
+//        c32 = 8 w .. 8 w + 7), levels 3-4 ((S0 + S1) + (S2 + S3)) across the 4 waves through LDS.
+// Block = 16 rows of W5 x 512 columns; wave w owns the columns 128 i + 32 w + [0, 32) (8 tiles of 16): lane (tl,
+// kq) holds row tl and, per tile, the columns base + 4 v + kq.  W5 comes into that layout (and dW5 out of it, for
+// RMSprop in the row layout of the 16-B accesses) through a wave-private LDS transpose once per block.
+// ------------------------------------------------------------------------------------------------
+constexpr int D5M_ROWS = 16;
+constexpr int D5M_SCHUNK = 16;          // samples staged at a time (one 16-sample tile)
+constexpr int D5M_DHS = HID + 20;       // dh row stride: conflict-free dd4 operand reads
+constexpr int D5M_XS = 128 + 4;         // transpose scratch row stride (a wave's 128 columns)
+constexpr int D5M_STAGE = D5M_SCHUNK * D5M_DHS;
+constexpr int D5M_LDS = (D5M_STAGE > 4 * 16 * D5M_XS) ? D5M_STAGE : 4 * 16 * D5M_XS;
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense5_bwd_mfma_kernel(
+    const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
+    float* __restrict__ rms, const float* __restrict__ glob, const int32_t* __restrict__ w5src,
+    float* __restrict__ dZ4, float lr, float rho, float omr, float decay, float eps) {
+  __shared__ float smem[D5M_LDS];
+  __shared__ float p_s[D5M_SCHUNK * D5M_ROWS];
+  __shared__ uint8_t c_s[D5M_SCHUNK * D5M_ROWS];
+  __shared__ float t_s[4 * 4 * 64];  // the waves' level-2 sums [w][v][lane]
+  float* const dh_s = smem;          // [sample][D5M_DHS]
+  const LogicalBlock lbk = xcd_block3();  // (row slice, replica): a replica's dh5 rows in one XCD's L2
+  const int r = lbk.y;
+  const int k0 = lbk.x * D5M_ROWS;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int tl = lane & 15, kq = lane >> 4;
+  float* const x_s = smem + wave * 16 * D5M_XS;  // this wave's transpose scratch (aliases the staging)
+  const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
+  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  // row layout: lane's fvec4 f = lane + 64 u (u = 0..7): row f / 32, column chunk i = (f % 32) / 8, columns
+  // 128 i + 32 w + 4 (f % 8) ..
+  auto rl_off = [&](int u) {
+    const int f = lane + 64 * u;
+    return (int64_t)(k0 + (f >> 5)) * HID + 128 * ((f & 31) >> 3) + 32 * wave + 4 * (f & 7);
+  };
+  const int gsrc = w5src ? w5src[r] : -1;
+  const float* Wsrc = gsrc >= 0 ? glob + (int64_t)gsrc * STRIDE + OFF_W5 : params + (int64_t)r * STRIDE + OFF_W5;
+  float* const Wr = params + (int64_t)r * STRIDE + OFF_W5;
+  float* const Rr = rms + (int64_t)r * STRIDE + OFF_W5;
+  fvec4 w[8], av[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    w[u] = *reinterpret_cast<const fvec4*>(Wsrc + rl_off(u));
+    av[u] = cfg.reset ? z4 : __builtin_nontemporal_load(reinterpret_cast<const fvec4*>(Rr + rl_off(u)));
+  }
+  // W5 into the MFMA layout: tile tau = 2 i + h (columns 128 i + 32 w + 16 h ..): wd[tau][v] = W5[tl][base + 4 v + kq]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int f = lane + 64 * u;
+    *reinterpret_cast<fvec4*>(x_s + (f >> 5) * D5M_XS + 32 * ((f & 31) >> 3) + 4 * (f & 7)) = w[u];
+  }
+  __syncthreads();
+  float wd[8][4];
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) wd[tau][v] = x_s[tl * D5M_XS + 16 * tau + 4 * v + kq];
+  fvec4 g[8];
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau) g[tau] = z4;
+  const float* Pr = D4 + (int64_t)r * bmax * FEAT;
+  const uint8_t* Cr = code4 + (int64_t)r * bmax * FEAT;
+  const float* dHr = dH + (int64_t)r * bmax * HID;
+  const int gcol = 4 * (tl & 3) + (tl >> 2);  // g's A row m = 4 a + b is column base + 4 b + a
+  for (int c0 = 0; c0 < count; c0 += D5M_SCHUNK) {
+    const int cn = min(D5M_SCHUNK, count - c0);
+    __syncthreads();  // the transpose reads / the previous chunk's readers are done
+    {
+      constexpr int HIT = D5M_SCHUNK * (HID / 4) / 256;
+      fvec4 hv[HIT];
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int e = tid + 256 * i;  // (sample e / 128, chunk e % 128)
+        const bool ok = e / (HID / 4) < cn;
+        const fvec4 t = *reinterpret_cast<const fvec4*>(dHr + (int64_t)(c0 + (ok ? e / (HID / 4) : 0)) * HID +
+                                                        4 * (e % (HID / 4)));
+        hv[i] = ok ? t : z4;
+      }
+      float pv = 0.0f;
+      uint8_t cv = 0;
+      {  // (sample tid / 16, row tid % 16)
+        const bool ok = tid / D5M_ROWS < cn;
+        const int64_t gi = (int64_t)(c0 + (ok ? tid / D5M_ROWS : 0)) * FEAT + k0 + tid % D5M_ROWS;
+        const float t = Pr[gi];
+        const uint8_t cc = Cr[gi];
+        pv = ok ? t : 0.0f;
+        cv = ok ? cc : (uint8_t)0;
+      }
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int e = tid + 256 * i;
+        float* d = dh_s + (e / (HID / 4)) * D5M_DHS + 4 * (e % (HID / 4));
+        d[0] = hv[i].x;
+        d[1] = hv[i].y;
+        d[2] = hv[i].z;
+        d[3] = hv[i].w;
+      }
+      p_s[tid] = pv;
+      c_s[tid] = cv;
+    }
+    __syncthreads();
+    // dW5: sample quads in order
+    for (int jq = 0; jq < cn; jq += 4) {
+      const float bp = p_s[(jq + kq) * D5M_ROWS + tl];
+      const float* dq = dh_s + (jq + kq) * D5M_DHS + 32 * wave + gcol;
+#pragma unroll
+      for (int tau = 0; tau < 8; ++tau) g[tau] = mfma16(dq[128 * (tau >> 1) + 16 * (tau & 1)], bp, g[tau]);
+    }
+    // dd4: per c32 = 8 w + c (columns 128 i + 32 w + 4 c + q) the chain over i, then tree levels 0-2
+    {
+      const float* da = dh_s + tl * D5M_DHS + 32 * wave + kq;
+      fvec4 pc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        pc[c] = z4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pc[c] = mfma16(da[128 * i + 4 * c], wd[2 * i + (c >> 2)][c & 3], pc[c]);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        t_s[(wave * 4 + v) * 64 + lane] =
+            ((pc[0][v] + pc[1][v]) + (pc[2][v] + pc[3][v])) + ((pc[4][v] + pc[5][v]) + (pc[6][v] + pc[7][v]));
+    }
+    __syncthreads();
+    {  // levels 3-4 across the waves; wave w finishes register v = w: sample 4 kq + w, row tl
+      const int v = wave;
+      const float d = (t_s[(0 * 4 + v) * 64 + lane] + t_s[(1 * 4 + v) * 64 + lane]) +
+                      (t_s[(2 * 4 + v) * 64 + lane] + t_s[(3 * 4 + v) * 64 + lane]);
+      const int jj = 4 * kq + v;
+      if (jj < cn) {  // dropout' and the pool's positive mask: the POOLED dz4 (conv4's gradients un-pool it)
+        const uint32_t c = c_s[jj * D5M_ROWS + tl];
+        const float dv = (c & CODE_KEEP) ? d * SCALE_25 : 0.0f;
+        dZ4[((int64_t)r * bmax + c0 + jj) * MPLC_CIFAR_DZ4 + k0 + tl] = (c & CODE_POS) ? dv : 0.0f;
+      }
+    }
+  }
+  __syncthreads();  // the last readers of the staging (and t_s) are done: the scratch takes dW5
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) x_s[tl * D5M_XS + 16 * tau + 4 * v + kq] = g[tau][v];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int f = lane + 64 * u;
+    const fvec4 gr = *reinterpret_cast<const fvec4*>(x_s + (f >> 5) * D5M_XS + 32 * ((f & 31) >> 3) + 4 * (f & 7));
+    fvec4 pw = w[u];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float p1 = pw[q], a1 = av[u][q];
+      rms_apply(p1, a1, gr[q], cfg);
+      pw[q] = p1;
+      av[u][q] = a1;
+    }
+    *reinterpret_cast<fvec4*>(Wr + rl_off(u)) = pw;
+    __builtin_nontemporal_store(av[u], reinterpret_cast<fvec4*>(Rr + rl_off(u)));
   }
   if (lbk.x == 0) {
     const float* dHs = dH + (int64_t)r * bmax * HID;
@@ -2146,9 +2331,15 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                                 t->lr, t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
   PROF_END(6);
   PROF_BEGIN(7);
+#if MPLC_D5_MFMA
+  dense5_bwd_mfma_kernel<<<dim3(FEAT / D5M_ROWS, R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B,
+                                                                  t->params, t->rms, t->glob, w5src, t->dz4, t->lr,
+                                                                  t->rho, t->one_minus_rho, t->decay, t->eps);
+#else
   dense5_bwd_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
                                                             t->rms, t->glob, w5src, t->dz4, t->lr, t->rho,
                                                             t->one_minus_rho, t->decay, t->eps);
+#endif
   PROF_END(7);
   // the data gradients' kernels (rotated, channels swapped) in Winograd form, over the forward's
   wino_u_kernel<1><<<dim3(7168 / 256, R), 256, 0, s>>>(t->params, STRIDE, t->cnt, t->wt);

@@ -666,6 +666,12 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 // Dense(128) backward + Adam, per 32-row slice of W3 (block = 256 threads: row = tid/8, 16 cols each)
 // dp[j][k] = sum_c dh[j][c] W3[k][c];  dW3[k][c] = sum_j p[j][k] dh[j][c];  db3 (slice 0 block)
 // ------------------------------------------------------------------------------------------------
+#ifndef MPLC_W1_LDS
+#define MPLC_W1_LDS 0  // conv_bwd_data / conv_wgrad read conv1's weights from an LDS copy (measured +0.5-0.9 %: off)
+#endif
+#ifndef MPLC_D1_MFMA
+#define MPLC_D1_MFMA 1  // dense1_bwd_adam_mfma_kernel (bit-identical MFMA form) instead of the VALU form
+#endif
 constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
 constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
@@ -782,6 +788,197 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
       } else {
         __builtin_nontemporal_store(mv[i], Mr + 8 * i);
         __builtin_nontemporal_store(vv[i], Vr + 8 * i);
+      }
+    }
+  }
+  if (k0 == 0 && tid < HID) {  // the replica's slice-0 block (logical order)
+    float gb = 0.0f;
+    const float* dHs = dH + (int64_t)r * bmax * HID;
+    for (int jj = 0; jj < count; ++jj) gb += dHs[(int64_t)jj * HID + tid];
+    const int64_t o = (int64_t)r * stride + OFF_B3 + tid;
+    adam_apply(params[o], adam_m[o], adam_v[o], gb, cfg);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The same pass with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense1_bwd_adam_kernel: the
+// matrix core accumulates D = C + sum_k A[m][k] B[k][n] as the fmaf chain k = 0, 1, 2, 3 (measured on every output
+// of 4096 random tiles, scripts/probes/mfma_order.hip), so MFMAs chained in the VALU loop's order reproduce it.
+//   dW3: the VALU form's chain per element runs over the samples in order (g += p_j dh_j): MFMA K = 4 samples,
+//        chained over sample quads; padded samples (zero p and dh) add exact zeros.
+//   dp:  the VALU form's thread c8 chains the 16 columns 4 c8 + 32 i + q (i outer, q inner) and the 8 partials
+//        are added in a fixed tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)): per c8 an MFMA chain over
+//        i with K = q (4 columns), then the same tree on the 8 accumulators, in registers.
+// Block = 64 rows of W3 (16 per wave) x all 128 columns.  In the MFMA layout lane (tl, kq) holds row tl and the
+// columns 16 tau + 4 v + kq (tau = 0..7, v = 0..3): W3 is brought into it (and dW3 out of it, for the Adam step in
+// the row layout of the coalesced 16-B accesses) through an LDS transpose once per block.  The VALU loop's 32
+// multiply-adds per sample and row-thread become 2 MFMAs per 4 samples per 16 x 16 tile; the pass is left with
+// its HBM traffic (W3, m, v read and written).
+// ------------------------------------------------------------------------------------------------
+constexpr int D1M_ROWS = 64;     // W3 rows per block (16 per wave)
+constexpr int D1M_SCHUNK = 32;   // samples staged in LDS at a time (two 16-sample tiles)
+constexpr int D1M_DHS = HID + 20;  // dh row stride: conflict-free for the dp operand reads (20 * m + kq)
+constexpr int D1M_PS = D1M_ROWS + 16;  // p row stride
+constexpr int D1M_XS = HID + 4;  // transpose scratch row stride (4 tl + kq: conflict-free)
+constexpr int D1M_STAGE = D1M_SCHUNK * (D1M_DHS + D1M_PS);
+constexpr int D1M_LDS = (D1M_STAGE > 4 * 16 * D1M_XS) ? D1M_STAGE : 4 * 16 * D1M_XS;
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_mfma_kernel(
+    const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
+    const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
+    float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
+  __shared__ float smem[D1M_LDS];
+  float* const dh_s = smem;                            // [sample][D1M_DHS]
+  float* const p_s = smem + D1M_SCHUNK * D1M_DHS;     // [sample][D1M_PS]
+  const int64_t lb = xcd_block();  // logical block (slice, r), replica-major: dh and p stay in one L2
+  const int r = (int)(lb / gridDim.x);
+  const int k0 = (int)(lb % gridDim.x) * D1M_ROWS;
+  const int count = cnt[r];
+  if (count == 0) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int tl = lane & 15, kq = lane >> 4;
+  float* const x_s = smem + wave * 16 * D1M_XS;  // this wave's transpose scratch [16 rows][D1M_XS] (aliases staging)
+  const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
+  const bool fresh = cfg.reset, second = (cfg.t == 2);  // moments as in dense1_bwd_adam_kernel
+  // row layout: lane's fvec4 f = lane + 64 u of the wave's 16 x 32 chunks (row f / 32, columns 4 (f % 32) ..)
+  const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + 16 * wave) * HID;
+  fvec4* W = reinterpret_cast<fvec4*>(params + roff) + lane;
+  const int gsrc = w3src ? w3src[r] : -1;
+  const fvec4* Wsrc = gsrc >= 0 ? reinterpret_cast<const fvec4*>(glob + roff + (int64_t)(gsrc - r) * stride) + lane : W;
+  fvec4* Mr = reinterpret_cast<fvec4*>(adam_m + roff) + lane;
+  fvec4* Vr = reinterpret_cast<fvec4*>(adam_v + roff) + lane;
+  const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  fvec4 w[8], mv[8], vv[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    w[u] = Wsrc[64 * u];
+    mv[u] = z4;
+    vv[u] = z4;
+  }
+  if (second) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mv[u] = __builtin_nontemporal_load(Mr + 64 * u);  // g1
+  } else if (!fresh) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mv[u] = __builtin_nontemporal_load(Mr + 64 * u);
+      vv[u] = __builtin_nontemporal_load(Vr + 64 * u);
+    }
+  }
+  // W3 into the MFMA layout: wd[tau][v] = W3[row tl][16 tau + 4 v + kq]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int f = lane + 64 * u;
+    *reinterpret_cast<fvec4*>(x_s + (f >> 5) * D1M_XS + 4 * (f & 31)) = w[u];
+  }
+  __syncthreads();
+  float wd[8][4];
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) wd[tau][v] = x_s[tl * D1M_XS + 16 * tau + 4 * v + kq];
+  fvec4 g[8];  // dW3 in the MFMA layout: g[tau][v] = row tl, column 16 tau + 4 v + kq
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau) g[tau] = z4;
+  const float* Pr = Pool + (int64_t)r * bmax * FEAT;
+  const float* dHr = dH + (int64_t)r * bmax * HID;
+  float* dPr = dPool + (int64_t)r * bmax * FEAT;
+  // operand columns: g's A row m = 4 a + b is column 16 tau + 4 b + a (the output's v <-> 4 v + kq)
+  const int gcol = 4 * (tl & 3) + (tl >> 2);
+  for (int c0 = 0; c0 < count; c0 += D1M_SCHUNK) {
+    const int cn = min(D1M_SCHUNK, count - c0);
+    __syncthreads();  // the transpose reads / the previous chunk's readers are done
+    {  // stage dh [32][128] and p [32][64] (zero past the chunk's samples: the padded MFMA steps add zeros)
+      constexpr int HIT = D1M_SCHUNK * (HID / 4) / 256, PIT = D1M_SCHUNK * (D1M_ROWS / 4) / 256;
+      fvec4 hv[HIT], pv[PIT];
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int e = tid + 256 * i;  // (sample e / 32, chunk e % 32)
+        const bool ok = e / (HID / 4) < cn;
+        const fvec4 t = *reinterpret_cast<const fvec4*>(dHr + (int64_t)(c0 + (ok ? e / (HID / 4) : 0)) * HID +
+                                                        4 * (e % (HID / 4)));
+        hv[i] = ok ? t : z4;
+      }
+#pragma unroll
+      for (int i = 0; i < PIT; ++i) {
+        const int e = tid + 256 * i;  // (sample e / 16, rows 4 (e % 16) ..)
+        const bool ok = e / (D1M_ROWS / 4) < cn;
+        const fvec4 t = *reinterpret_cast<const fvec4*>(Pr + (int64_t)(c0 + (ok ? e / (D1M_ROWS / 4) : 0)) * FEAT +
+                                                        k0 + 4 * (e % (D1M_ROWS / 4)));
+        pv[i] = ok ? t : z4;
+      }
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int e = tid + 256 * i;
+        float* d = dh_s + (e / (HID / 4)) * D1M_DHS + 4 * (e % (HID / 4));
+        d[0] = hv[i].x;
+        d[1] = hv[i].y;
+        d[2] = hv[i].z;
+        d[3] = hv[i].w;
+      }
+#pragma unroll
+      for (int i = 0; i < PIT; ++i) {
+        const int e = tid + 256 * i;
+        *reinterpret_cast<fvec4*>(p_s + (e / (D1M_ROWS / 4)) * D1M_PS + 4 * (e % (D1M_ROWS / 4))) = pv[i];
+      }
+    }
+    __syncthreads();
+    // dW3: sample quads in order
+    for (int jq = 0; jq < cn; jq += 4) {
+      const float bp = p_s[(jq + kq) * D1M_PS + 16 * wave + tl];
+      const float* dq = dh_s + (jq + kq) * D1M_DHS + gcol;
+#pragma unroll
+      for (int tau = 0; tau < 8; ++tau) g[tau] = mfma16(dq[16 * tau], bp, g[tau]);
+    }
+    // dp: 16-sample tiles; per c8 the chain over i (K = 4 columns), then the VALU form's tree
+    for (int j0 = 0; j0 < cn; j0 += 16) {
+      const float* da = dh_s + (j0 + tl) * D1M_DHS + kq;
+      fvec4 pc[8];
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8) {
+        pc[c8] = z4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // column 4 c8 + 32 i + kq = 16 (c8 / 4 + 2 i) + 4 (c8 % 4) + kq
+          pc[c8] = mfma16(da[4 * c8 + 32 * i], wd[c8 / 4 + 2 * i][c8 % 4], pc[c8]);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {  // lane holds sample j0 + 4 kq + v, row tl
+        const float d = ((pc[0][v] + pc[1][v]) + (pc[2][v] + pc[3][v])) + ((pc[4][v] + pc[5][v]) + (pc[6][v] + pc[7][v]));
+        const int jj = j0 + 4 * kq + v;
+        if (jj < cn) dPr[(int64_t)(c0 + jj) * FEAT + k0 + 16 * wave + tl] = d;
+      }
+    }
+  }
+  // dW3 back to the row layout through the scratch (which aliases the staging: wait for its last readers)
+  __syncthreads();
+#pragma unroll
+  for (int tau = 0; tau < 8; ++tau)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) x_s[tl * D1M_XS + 16 * tau + 4 * v + kq] = g[tau][v];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int f = lane + 64 * u;
+    const fvec4 gr = *reinterpret_cast<const fvec4*>(x_s + (f >> 5) * D1M_XS + 4 * (f & 31));
+    fvec4 pw = w[u];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float p1 = pw[q], m1 = mv[u][q], v1 = vv[u][q];
+      if (second) adam_first_moments(mv[u][q], cfg, m1, v1);
+      adam_apply(p1, m1, v1, gr[q], cfg);
+      pw[q] = p1;
+      mv[u][q] = m1;
+      vv[u][q] = v1;
+    }
+    W[64 * u] = pw;
+    if (!cfg.last) {
+      if (fresh) {
+        __builtin_nontemporal_store(gr, Mr + 64 * u);
+      } else {
+        __builtin_nontemporal_store(mv[u], Mr + 64 * u);
+        __builtin_nontemporal_store(vv[u], Vr + 64 * u);
       }
     }
   }
@@ -925,7 +1122,8 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   load_img(j_begin);
   // conv1's weights for the epilogue: read here, where their latency hides behind the first quarter's staging,
   // instead of from global memory at the epilogue's start (one exposed load round trip per block)
-  for (int e = tid; e < 10 * C1; e += BWD_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
+  if (MPLC_W1_LDS)
+    for (int e = tid; e < 10 * C1; e += BWD_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
   {
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
@@ -1073,7 +1271,10 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = 4 * s3 + kq, ci = 16 * h + tl;
-      w1b[s3][h] = (k < 10) ? w1_s[k * C1 + ci] : 0.0f;
+      if (MPLC_W1_LDS)
+        w1b[s3][h] = (k < 10) ? w1_s[k * C1 + ci] : 0.0f;
+      else
+        w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
     }
   fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
   fvec4 gacc1 = gacc;
@@ -1208,7 +1409,8 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const float* P = params + (int64_t)r * stride;
   float w1r[5];
   load_w1r(P, kh, m, w1r);
-  for (int e = tid; e < 10 * C1; e += WG_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
+  if (MPLC_W1_LDS)
+    for (int e = tid; e < 10 * C1; e += WG_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
   float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread stages has that channel)
   float pdv[WG_PRE];
   uint32_t pcd[WG_PRE];
@@ -1291,7 +1493,9 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int s3 = 0; s3 < 3; ++s3) {
           const int k = 4 * s3 + kq;
           const float av = (k < 9) ? img_s[(4 * band + p / A1 + k / 3) * IMG + p % A1 + k % 3] : ((k == 9) ? 1.0f : 0.0f);
-          const float wv = (k < 10) ? w1_s[k * C1 + 16 * h + tl] : 0.0f;
+          const float wv = MPLC_W1_LDS ? ((k < 10) ? w1_s[k * C1 + 16 * h + tl] : 0.0f)
+                                       : ((k < 9) ? P[OFF_W1 + k * C1 + 16 * h + tl]
+                                                  : ((k == 9) ? P[OFF_B1 + 16 * h + tl] : 0.0f));
           c1 = mfma16(av, wv, c1);
         }
 #pragma unroll
@@ -1574,10 +1778,17 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                 S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps, t->hstats);
   PROF_END(3);
   PROF_BEGIN(4);
+#if MPLC_D1_MFMA
+  dense1_bwd_adam_mfma_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+                                                                       t->params, t->adam_m, t->adam_v, S, t->glob,
+                                                                       w3src, t->dpooled,
+                                                                       t->lr, t->beta1, t->beta2, t->eps);
+#else
   dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                   t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                   w3src, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
+#endif
   PROF_END(4);
   }
   if (ph & MPLC_PHASE_BACK) {
