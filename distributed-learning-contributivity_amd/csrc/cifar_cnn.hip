@@ -636,6 +636,9 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
+#ifndef MPLC_FWD_BIAS_PRE
+#define MPLC_FWD_BIAS_PRE 1  // forward epilogues: bias loaded ahead (wave-local: last k-step; row form: LDS)
+#endif
 #ifndef MPLC_ROW_EPI_STAGE
 #define MPLC_ROW_EPI_STAGE 1  // wino_kernel: the data gradients' epilogue operand staged as bytes in LDS up front
 #endif
@@ -666,6 +669,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ float in_s[LR * ROWP];
   __shared__ float t_s[8 * TQ];
   __shared__ uint32_t e_s[STAGE_EPI ? ER * WO * CO / 4 : 1];
+  constexpr bool STAGE_BIAS = MPLC_FWD_BIAS_PRE && (EPI == EPI_FWD || POOL);
+  __shared__ float b_s[STAGE_BIAS ? CO : 1];  // the forward's bias, staged with the input band
   const LogicalBlock lbk = xcd_block3();  // (band, sample, replica): a replica's blocks share one XCD's L2 (its U)
   const int band = lbk.x, j = lbk.y, r = lbk.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
@@ -707,6 +712,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         d[3] = v[k].w;
       }
     }
+  }
+  if constexpr (STAGE_BIAS) {
+    if (tid < CO) b_s[tid] = a.bias[(int64_t)r * a.b_rstride + tid];
   }
   if constexpr (STAGE_EPI) {
     constexpr int TOT = ER * WO * (CO / 4);
@@ -851,7 +859,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (tt < ntile) {
           const int ty = ty0 + tt / TXT, tx2 = tt % TXT;
           if constexpr (POOL) {
-            const float bv = bias[co];
+            const float bv = STAGE_BIAS ? b_s[STAGE_BIAS ? co : 0] : bias[co];
             float best = y[0] + bv;
             int arg = 0;
 #pragma unroll
@@ -875,7 +883,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               if (yy >= HO || xx >= WO) continue;
               const int o_i = (yy * WO + xx) * CO + co;
               if constexpr (EPI == EPI_FWD) {
-                o[o_i] = fmaxf(y[q] + bias[co], 0.0f);
+                o[o_i] = fmaxf(y[q] + (STAGE_BIAS ? b_s[STAGE_BIAS ? co : 0] : bias[co]), 0.0f);
               } else if constexpr (EPI == EPI_BWD_MASK) {
                 if constexpr (STAGE_EPI) {
                   o[o_i] = reinterpret_cast<const uint8_t*>(e_s)[((yy - 2 * ty0) * WO + xx) * CO + co] ? y[q] : 0.0f;
@@ -1244,6 +1252,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
     }
   };
+  // EPI_FWD_POOL: the lane's two bias values likewise (MPLC_FWD_BIAS_PRE)
+  constexpr bool PRE_BIAS = POOL && MPLC_FWD_BIAS_PRE;
+  float bpre[2] = {0.0f, 0.0f};
   float b0[32], b1[32];
   load_b(0, b0);
   static_assert(NK % 2 == 0 && NK >= 2, "k-steps in pairs");
@@ -1258,11 +1269,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   load_b(NK - 1, b1);
   kstep(NK - 2, b0);
   if constexpr (PRE_MASK) load_mask();
+  if constexpr (PRE_BIAS) {
+    bpre[0] = a.bias[(int64_t)r * a.b_rstride + tl];
+    bpre[1] = a.bias[(int64_t)r * a.b_rstride + 16 + tl];
+  }
   kstep(NK - 1, b1);
   if constexpr (PRE_MASK) {  // the loads stay ahead of the last k-step (not sunk to their use)
 #pragma unroll
     for (int i = 0; i < 8 * PRE_RR; ++i) asm volatile("" : "+v"(mk[i]));
   }
+  if constexpr (PRE_BIAS) asm volatile("" : "+v"(bpre[0]), "+v"(bpre[1]));
   // output transform in registers: lane holds M[xi][tile 4 kq + rr][co 16 cg + tl]
   float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
   const uint32_t rseed = (POOL && a.drop_key) ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
@@ -1288,7 +1304,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       y[2] = (tv[1][0] - tv[2][0]) - tv[3][0];
       y[3] = (tv[1][1] - tv[2][1]) - tv[3][1];
       if constexpr (POOL) {
-        const float bv = a.bias[(int64_t)r * a.b_rstride + co];
+        const float bv = PRE_BIAS ? bpre[cg] : a.bias[(int64_t)r * a.b_rstride + co];
         float best = y[0] + bv;
         int arg = 0;
 #pragma unroll
@@ -1787,7 +1803,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 // fresh optimizer's first step).
 // ------------------------------------------------------------------------------------------------
 #ifndef MPLC_D5_MFMA
-#define MPLC_D5_MFMA 1  // dense5_bwd_mfma_kernel (bit-identical MFMA form) instead of the VALU form
+#define MPLC_D5_MFMA 1  // dense5_bwd_kernel (bit-identical MFMA form) instead of the VALU form
 #endif
 constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
 #ifndef MPLC_D5_GROUPS
@@ -1799,7 +1815,7 @@ constexpr int D5_GROUPS = MPLC_D5_GROUPS;  // row groups per block
 #endif
 constexpr int D5_SCHUNK = MPLC_D5_SCHUNK;  // samples staged at a time
 
-__global__ __launch_bounds__(256) void dense5_bwd_kernel(
+__global__ __launch_bounds__(256) void dense5_bwd_valu_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
     const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
     float* __restrict__ rms, const float* __restrict__ glob, const int32_t* __restrict__ w5src,
@@ -1932,9 +1948,9 @@ __global__ __launch_bounds__(256) void dense5_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// dense5_bwd with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense5_bwd_kernel (the matrix core
+// dense5_bwd with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense5_bwd_valu_kernel (the matrix core
 // accumulates as the fmaf chain in k order, scripts/probes/mfma_order.hip; same reasoning as mnist_cnn.hip's
-// dense1_bwd_adam_mfma_kernel):
+// dense1_bwd_adam_kernel):
 //   dW5: the VALU chain over the samples in order -> MFMA K = 4 samples chained over sample quads;
 //   dd4: the VALU form's 32 partials (lane c32 of a row: columns 4 c32 + 128 i + q, i outer, q inner) -> per c32
 //        an MFMA chain over i with K = q, then the same 5-level tree over c32: levels 0-2 in registers (a wave owns
@@ -1950,7 +1966,7 @@ constexpr int D5M_XS = 128 + 4;         // transpose scratch row stride (a wave'
 constexpr int D5M_STAGE = D5M_SCHUNK * D5M_DHS;
 constexpr int D5M_LDS = (D5M_STAGE > 4 * 16 * D5M_XS) ? D5M_STAGE : 4 * 16 * D5M_XS;
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense5_bwd_mfma_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense5_bwd_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
     const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t, int bmax, float* __restrict__ params,
     float* __restrict__ rms, const float* __restrict__ glob, const int32_t* __restrict__ w5src,
@@ -2332,11 +2348,11 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
   PROF_END(6);
   PROF_BEGIN(7);
 #if MPLC_D5_MFMA
-  dense5_bwd_mfma_kernel<<<dim3(FEAT / D5M_ROWS, R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B,
+  dense5_bwd_kernel<<<dim3(FEAT / D5M_ROWS, R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B,
                                                                   t->params, t->rms, t->glob, w5src, t->dz4, t->lr,
                                                                   t->rho, t->one_minus_rho, t->decay, t->eps);
 #else
-  dense5_bwd_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
+  dense5_bwd_valu_kernel<<<dim3(FEAT / (D5_ROWS * D5_GROUPS), R), 256, 0, s>>>(t->d4, t->code4, t->dh5, t->cnt, t->opt_t, B, t->params,
                                                             t->rms, t->glob, w5src, t->dz4, t->lr, t->rho,
                                                             t->one_minus_rho, t->decay, t->eps);
 #endif

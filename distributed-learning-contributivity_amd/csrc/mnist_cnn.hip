@@ -670,12 +670,12 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 #define MPLC_W1_LDS 0  // conv_bwd_data / conv_wgrad read conv1's weights from an LDS copy (measured +0.5-0.9 %: off)
 #endif
 #ifndef MPLC_D1_MFMA
-#define MPLC_D1_MFMA 1  // dense1_bwd_adam_mfma_kernel (bit-identical MFMA form) instead of the VALU form
+#define MPLC_D1_MFMA 1  // dense1_bwd_adam_kernel (bit-identical MFMA form) instead of the VALU form
 #endif
 constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
 constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
-__global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
+__global__ __launch_bounds__(256) void dense1_bwd_adam_valu_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
@@ -801,7 +801,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// The same pass with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense1_bwd_adam_kernel: the
+// The same pass with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense1_bwd_adam_valu_kernel: the
 // matrix core accumulates D = C + sum_k A[m][k] B[k][n] as the fmaf chain k = 0, 1, 2, 3 (measured on every output
 // of 4096 random tiles, scripts/probes/mfma_order.hip), so MFMAs chained in the VALU loop's order reproduce it.
 //   dW3: the VALU form's chain per element runs over the samples in order (g += p_j dh_j): MFMA K = 4 samples,
@@ -823,7 +823,7 @@ constexpr int D1M_XS = HID + 4;  // transpose scratch row stride (4 tl + kq: con
 constexpr int D1M_STAGE = D1M_SCHUNK * (D1M_DHS + D1M_PS);
 constexpr int D1M_LDS = (D1M_STAGE > 4 * 16 * D1M_XS) ? D1M_STAGE : 4 * 16 * D1M_XS;
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_mfma_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int tl = lane & 15, kq = lane >> 4;
   float* const x_s = smem + wave * 16 * D1M_XS;  // this wave's transpose scratch [16 rows][D1M_XS] (aliases staging)
   const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
-  const bool fresh = cfg.reset, second = (cfg.t == 2);  // moments as in dense1_bwd_adam_kernel
+  const bool fresh = cfg.reset, second = (cfg.t == 2);  // moments as in dense1_bwd_adam_valu_kernel
   // row layout: lane's fvec4 f = lane + 64 u of the wave's 16 x 32 chunks (row f / 32, columns 4 (f % 32) ..)
   const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + 16 * wave) * HID;
   fvec4* W = reinterpret_cast<fvec4*>(params + roff) + lane;
@@ -1779,12 +1779,12 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   PROF_END(3);
   PROF_BEGIN(4);
 #if MPLC_D1_MFMA
-  dense1_bwd_adam_mfma_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+  dense1_bwd_adam_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                        t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                        w3src, t->dpooled,
                                                                        t->lr, t->beta1, t->beta2, t->eps);
 #else
-  dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+  dense1_bwd_adam_valu_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                   t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                   w3src, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
