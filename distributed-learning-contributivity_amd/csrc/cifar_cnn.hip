@@ -636,6 +636,13 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
+#ifndef MPLC_ROW_WSPEC
+#define MPLC_ROW_WSPEC 1  // wino_kernel: the group loop compiled per wave (compile-time B^T signs)
+#endif
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 #ifndef MPLC_FWD_BIAS_PRE
 #define MPLC_FWD_BIAS_PRE 1  // forward epilogues: bias loaded ahead (wave-local: last k-step; row form: LDS)
 #endif
@@ -752,12 +759,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int lane = tid & 63, wave = tid >> 6;
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
-  // B^T row i combines patch rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  const int drow = (rb - ra) * ROWP;
   // B operands of k-step st: U[4 wi + jj][4 st + kq][16 cg + tl] (the xi-first layout: a 16-lane group reads 64
   // contiguous bytes per transform point; the xi-last layout's one 16-B load per channel pair measured 5-10 % slower
   // here, scripts/r04/gpu_ab_cifar.sh)
@@ -784,6 +785,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int st = 0; st < KR; ++st) load_b(st, bw[st]);
   __syncthreads();
+  // The group loop, compiled once per wave (MPLC_ROW_WSPEC): B^T row i combines patch rows (ra, rb) with signs
+  // (sa, sb), t = sa*d[ra] + sb*d[rb]; with the wave's row a compile-time constant that is one add or subtract per
+  // value instead of a multiply and a multiply-add (the products by +-1 are exact: the same values either way)
+  auto groups = [&](auto wtag) __attribute__((always_inline)) {
+  constexpr int WIC = decltype(wtag)::value;
+  const int ra = WIC >= 0 ? (WIC == 0 ? 0 : 1) : (wi == 0 ? 0 : 1);
+  const int rb = WIC >= 0 ? (WIC == 3 ? 3 : 2) : (wi == 3 ? 3 : 2);
+  const float sa = WIC >= 0 ? (WIC == 2 ? -1.0f : 1.0f) : (wi == 2 ? -1.0f : 1.0f);
+  const float sb = WIC >= 0 ? ((WIC == 0 || WIC == 3) ? -1.0f : 1.0f) : ((wi == 0 || wi == 3) ? -1.0f : 1.0f);
+  const int drow = (rb - ra) * ROWP;
 #pragma unroll 1
   for (int g = 0; g < NG; ++g) {
     if (16 * g >= ntile) break;  // block-uniform
@@ -801,7 +812,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const float* d0 = dpa + 4 * st;
       float t[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * CIP] + sb * d0[drow + c * CIP];
+      for (int c = 0; c < 4; ++c) {
+        if constexpr (WIC >= 0) {
+          const float da = d0[c * CIP], db = d0[drow + c * CIP];
+          t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+        } else {
+          t[c] = sa * d0[c * CIP] + sb * d0[drow + c * CIP];
+        }
+      }
       float v[4];
       v[0] = t[0] - t[2];
       v[1] = t[1] + t[2];
@@ -904,6 +922,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __syncthreads();
     }
   }
+  };
+  if constexpr (MPLC_ROW_WSPEC) {
+    switch (wi) {  // wave-uniform
+      case 0: groups(IntC<0>{}); break;
+      case 1: groups(IntC<1>{}); break;
+      case 2: groups(IntC<2>{}); break;
+      default: groups(IntC<3>{}); break;
+    }
+  } else {
+    groups(IntC<-1>{});
+  }
+
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1391,13 +1421,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int lane = tid & 63, wave = tid >> 6;
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  const float ai0 = (wi == 3) ? 0.0f : 1.0f;                       // A[i][0]
-  const float ai1 = (wi == 0) ? 0.0f : ((wi == 1) ? 1.0f : -1.0f);  // A[i][1]
-  const int drow = (rb - ra) * XROW;
   fvec4 acc[4][NH][NCG];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj)
@@ -1406,6 +1429,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fvec4 gb = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // db partial of channels 4 * (tid % (CO / 4)) .. + 3
+  // the sample loop compiled once per wave (MPLC_ROW_WSPEC, as in wino_kernel): the wave's transform row fixes the
+  // signs of B^T (sa, sb) and A (ai0, ai1), so V and D take adds / subtracts / moves instead of multiplies by 0 / +-1
+  auto samples = [&](auto wtag) __attribute__((always_inline)) {
+  constexpr int WIC = decltype(wtag)::value;
+  const int wv = WIC >= 0 ? WIC : wi;
+  const int ra = (wv == 0) ? 0 : 1;
+  const int rb = (wv == 3) ? 3 : 2;
+  const float sa = (wv == 2) ? -1.0f : 1.0f;
+  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
+  const float ai0 = (wv == 3) ? 0.0f : 1.0f;                       // A[i][0]
+  const float ai1 = (wv == 0) ? 0.0f : ((wv == 1) ? 1.0f : -1.0f);  // A[i][1]
+  const int drow = (rb - ra) * XROW;
   for (int j = j_begin; j < j_end; ++j) {
     const int64_t slot = (int64_t)r * a.bmax + j;
     const float* X = a.x + slot * (HI * WI * CI) + chn * CIB;
@@ -1502,7 +1537,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int h = 0; h < NH; ++h) {
           float t[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) t[c] = sa * d0[c * CIP + 16 * h] + sb * d0[drow + c * CIP + 16 * h];
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (WIC >= 0) {
+              const float da = d0[c * CIP + 16 * h], db = d0[drow + c * CIP + 16 * h];
+              t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+            } else {
+              t[c] = sa * d0[c * CIP + 16 * h] + sb * d0[drow + c * CIP + 16 * h];
+            }
+          }
           va[h][0] = ok ? t[0] - t[2] : 0.0f;
           va[h][1] = ok ? t[1] + t[2] : 0.0f;
           va[h][2] = ok ? t[2] - t[1] : 0.0f;
@@ -1514,7 +1556,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int cg = 0; cg < NCG; ++cg) {
           const float y00 = z0[16 * cg], y01 = z0[COP + 16 * cg];
           const float y10 = z0[ZC * COP + 16 * cg], y11 = z0[ZC * COP + COP + 16 * cg];
-          const float r0 = ai0 * y00 + ai1 * y10, r1 = ai0 * y01 + ai1 * y11;  // row i of A dY
+          float r0, r1;  // row i of A dY
+          if constexpr (WIC == 0) {
+            r0 = y00;
+            r1 = y01;
+          } else if constexpr (WIC == 1) {
+            r0 = y00 + y10;
+            r1 = y01 + y11;
+          } else if constexpr (WIC == 2) {
+            r0 = y00 - y10;
+            r1 = y01 - y11;
+          } else if constexpr (WIC == 3) {
+            r0 = -y10;
+            r1 = -y11;
+          } else {
+            r0 = ai0 * y00 + ai1 * y10;
+            r1 = ai0 * y01 + ai1 * y11;
+          }
           db[cg][0] = r0;
           db[cg][1] = r0 + r1;
           db[cg][2] = r0 - r1;
@@ -1528,6 +1586,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = mfma16(va[h][jj], db[cg][jj], acc[jj][h][cg]);
       }
     }
+  }
+  };
+  if constexpr (MPLC_ROW_WSPEC) {
+    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
+      case 0: samples(IntC<0>{}); break;
+      case 1: samples(IntC<1>{}); break;
+      case 2: samples(IntC<2>{}); break;
+      default: samples(IntC<3>{}); break;
+    }
+  } else {
+    samples(IntC<-1>{});
   }
   // inverse transform dW[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]; lane holds
   // ci 16 h + 4 kq + rr (of the chunk), co 16 cg + tl
@@ -1950,7 +2019,7 @@ __global__ __launch_bounds__(256) void dense5_bwd_valu_kernel(
 // ------------------------------------------------------------------------------------------------
 // dense5_bwd with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense5_bwd_valu_kernel (the matrix core
 // accumulates as the fmaf chain in k order, scripts/probes/mfma_order.hip; same reasoning as mnist_cnn.hip's
-// dense1_bwd_adam_kernel):
+// dense1_bwd_adam_mfma_kernel):
 //   dW5: the VALU chain over the samples in order -> MFMA K = 4 samples chained over sample quads;
 //   dd4: the VALU form's 32 partials (lane c32 of a row: columns 4 c32 + 128 i + q, i outer, q inner) -> per c32
 //        an MFMA chain over i with K = q, then the same 5-level tree over c32: levels 0-2 in registers (a wave owns

@@ -25,6 +25,17 @@
 #include "keyed.h"
 #include "xcd.h"
 
+#ifndef MPLC_WSPEC
+#define MPLC_WSPEC 1  // conv_wgrad: the sample loop compiled per wave (compile-time transform signs)
+#endif
+#ifndef MPLC_WSPEC_FWD
+#define MPLC_WSPEC_FWD 1  // conv_fwd likewise
+#endif
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+
 // Timing-experiment switches compile parts of a kernel out and give WRONG results by design (A/B probes of
 // where a kernel's time goes).  A product build must never carry one.
 #if (defined(BWD_EXP_NOSTAGE) || defined(BWD_EXP_NOSTAGE_UR) || defined(BWD_EXP_NOSTAGE_DZ) || \
@@ -289,11 +300,6 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
   // B^T row i combines input rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  const int drow = (rb - ra) * A1 * A1P;
   // the wave's B operands of all 8 k-steps (its transform row of U), resident for the whole block
   const float* Ub = U + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C1 * C2 + kq * C2 + tl;
   const float bias = P[OFF_B2 + (tid & 63)];  // the output phase's channel co = tid & 63 in every pass
@@ -312,6 +318,16 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   store_img(img_s[0]);
   if (j_begin + 1 < j_end) load_img(j_begin + 1);  // in flight during the first sample
   __syncthreads();
+  // the sample loop compiled once per wave (MPLC_WSPEC): the wave's transform row i fixes B^T's signs, so V takes
+  // one add / subtract per value instead of a multiply and a multiply-add (products by +-1 are exact: same values)
+  auto samples = [&](auto wtag) __attribute__((always_inline)) {
+  constexpr int WIC = decltype(wtag)::value;
+  const int wv = WIC >= 0 ? WIC : wi;
+  const int ra = (wv == 0) ? 0 : 1;
+  const int rb = (wv == 3) ? 3 : 2;
+  const float sa = (wv == 2) ? -1.0f : 1.0f;
+  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
+  const int drow = (rb - ra) * A1 * A1P;
 #pragma unroll 1
   for (int j = j_begin; j < j_end; ++j) {
     // a1_s is free (the previous sample's last two barriers follow its last GEMM read); this sample's image is
@@ -364,7 +380,12 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       auto make_v = [&](float (&v)[4]) {
         float t[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = sa * pn[c] + sb * pn[4 + c];
+        for (int c = 0; c < 4; ++c) {
+          if constexpr (WIC >= 0)
+            t[c] = (WIC == 2 ? -pn[c] : pn[c]) + (WIC == 0 || WIC == 3 ? -pn[4 + c] : pn[4 + c]);
+          else
+            t[c] = sa * pn[c] + sb * pn[4 + c];
+        }
         v[0] = t[0] - t[2];
         v[1] = t[1] + t[2];
         v[2] = t[2] - t[1];
@@ -432,6 +453,17 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       }
       __syncthreads();
     }
+  }
+  };
+  if constexpr (MPLC_WSPEC_FWD) {
+    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
+      case 0: samples(IntC<0>{}); break;
+      case 1: samples(IntC<1>{}); break;
+      case 2: samples(IntC<2>{}); break;
+      default: samples(IntC<3>{}); break;
+    }
+  } else {
+    samples(IntC<-1>{});
   }
 }
 
@@ -670,12 +702,13 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 #define MPLC_W1_LDS 0  // conv_bwd_data / conv_wgrad read conv1's weights from an LDS copy (measured +0.5-0.9 %: off)
 #endif
 #ifndef MPLC_D1_MFMA
-#define MPLC_D1_MFMA 1  // dense1_bwd_adam_kernel (bit-identical MFMA form) instead of the VALU form
+#define MPLC_D1_MFMA 0  // dense1_bwd_adam_mfma_kernel (bit-identical MFMA form) instead of the VALU form: -4.7 % on the
+                        // 1260-replica probe but +1.9 % at the bench's 5120 replicas (memory-bound there), so off
 #endif
 constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
 constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
-__global__ __launch_bounds__(256) void dense1_bwd_adam_valu_kernel(
+__global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
@@ -801,7 +834,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_valu_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// The same pass with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense1_bwd_adam_valu_kernel: the
+// The same pass with both products on v_mfma_f32_16x16x4_f32, bit-identical to dense1_bwd_adam_kernel: the
 // matrix core accumulates D = C + sum_k A[m][k] B[k][n] as the fmaf chain k = 0, 1, 2, 3 (measured on every output
 // of 4096 random tiles, scripts/probes/mfma_order.hip), so MFMAs chained in the VALU loop's order reproduce it.
 //   dW3: the VALU form's chain per element runs over the samples in order (g += p_j dh_j): MFMA K = 4 samples,
@@ -823,7 +856,7 @@ constexpr int D1M_XS = HID + 4;  // transpose scratch row stride (4 tl + kq: con
 constexpr int D1M_STAGE = D1M_SCHUNK * (D1M_DHS + D1M_PS);
 constexpr int D1M_LDS = (D1M_STAGE > 4 * 16 * D1M_XS) ? D1M_STAGE : 4 * 16 * D1M_XS;
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_mfma_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
@@ -841,7 +874,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int tl = lane & 15, kq = lane >> 4;
   float* const x_s = smem + wave * 16 * D1M_XS;  // this wave's transpose scratch [16 rows][D1M_XS] (aliases staging)
   const AdamCfg cfg = adam_cfg(adam_t[r], lr, b1, b2, eps);
-  const bool fresh = cfg.reset, second = (cfg.t == 2);  // moments as in dense1_bwd_adam_valu_kernel
+  const bool fresh = cfg.reset, second = (cfg.t == 2);  // moments as in dense1_bwd_adam_kernel
   // row layout: lane's fvec4 f = lane + 64 u of the wave's 16 x 32 chunks (row f / 32, columns 4 (f % 32) ..)
   const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + 16 * wave) * HID;
   fvec4* W = reinterpret_cast<fvec4*>(params + roff) + lane;
@@ -1439,12 +1472,6 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const int tl = lane & 15, kq = lane >> 4;
   // B^T row i (input transform) combines patch rows (ra, rb) with signs (sa, sb); A row i (gradient
   // transform) picks delta's row dy with factor A[i][dy]
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  const float ai0 = (wi == 3) ? 0.0f : 1.0f;                       // A[i][0]
-  const float ai1 = (wi == 0) ? 0.0f : ((wi == 1) ? 1.0f : -1.0f);  // A[i][1]
   fvec4 acc[4][2][4];  // [j][ci half][co group]
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj)
@@ -1454,6 +1481,16 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fetch(j_begin, 0);
   fetch_img(j_begin);
+  // the sample loop compiled once per wave (MPLC_WSPEC): signs of B^T and A's row are compile-time constants
+  auto samples = [&](auto wtag) __attribute__((always_inline)) {
+  constexpr int WIC = decltype(wtag)::value;
+  const int wv = WIC >= 0 ? WIC : wi;
+  const int ra = (wv == 0) ? 0 : 1;
+  const int rb = (wv == 3) ? 3 : 2;
+  const float sa = (wv == 2) ? -1.0f : 1.0f;
+  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
+  const float ai0 = (wv == 3) ? 0.0f : 1.0f;                       // A[i][0]
+  const float ai1 = (wv == 0) ? 0.0f : ((wv == 1) ? 1.0f : -1.0f);  // A[i][1]
   for (int j = j_begin; j < j_end; ++j) {
     for (int band = 0; band < 6; ++band) {
       __syncthreads();  // previous band's readers (a1_s, vq_s; and img_s by its staging) done
@@ -1531,7 +1568,12 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int ch = 0; ch < 2; ++ch) {
           float t[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) t[c] = sa * pa[c][ch] + sb * pb[c][ch];
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (WIC >= 0)
+              t[c] = (WIC == 2 ? -pa[c][ch] : pa[c][ch]) + (WIC == 0 || WIC == 3 ? -pb[c][ch] : pb[c][ch]);
+            else
+              t[c] = sa * pa[c][ch] + sb * pb[c][ch];
+          }
           va[ch][0] = t[0] - t[2];
           va[ch][1] = t[1] + t[2];
           va[ch][2] = t[2] - t[1];
@@ -1544,7 +1586,12 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
           const int2 vs = vq_s[tb * WG_VS + 16 * cg + tl];
           const float v = __int_as_float(vs.x);
           const int sl = vs.y;
-          const float vi = ((sl & 2) ? ai1 : ai0) * v;
+          float vi;
+          if constexpr (WIC == 0) vi = (sl & 2) ? 0.0f : v;
+          else if constexpr (WIC == 1) vi = v;
+          else if constexpr (WIC == 2) vi = (sl & 2) ? -v : v;
+          else if constexpr (WIC == 3) vi = (sl & 2) ? -v : 0.0f;
+          else vi = ((sl & 2) ? ai1 : ai0) * v;
           const bool dx = (sl & 1) != 0;
           db[cg][0] = dx ? 0.0f : vi;
           db[cg][1] = vi;
@@ -1559,6 +1606,17 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
             for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = mfma16(va[ch][jj], db[cg][jj], acc[jj][ch][cg]);
       }
     }
+  }
+  };
+  if constexpr (MPLC_WSPEC) {
+    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
+      case 0: samples(IntC<0>{}); break;
+      case 1: samples(IntC<1>{}); break;
+      case 2: samples(IntC<2>{}); break;
+      default: samples(IntC<3>{}); break;
+    }
+  } else {
+    samples(IntC<-1>{});
   }
   // inverse transform dW2[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]: wave i folds
   // its row (P_i0 = M_i0 + .5 M_i1 + .5 M_i2, P_i1 = .5 M_i1 - .5 M_i2, P_i2 = .5 M_i1 + .5 M_i2 + M_i3), the
@@ -1779,12 +1837,12 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   PROF_END(3);
   PROF_BEGIN(4);
 #if MPLC_D1_MFMA
-  dense1_bwd_adam_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+  dense1_bwd_adam_mfma_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                        t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                        w3src, t->dpooled,
                                                                        t->lr, t->beta1, t->beta2, t->eps);
 #else
-  dense1_bwd_adam_valu_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
+  dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                   t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                   w3src, t->dpooled,
                                                                   t->lr, t->beta1, t->beta2, t->eps);
