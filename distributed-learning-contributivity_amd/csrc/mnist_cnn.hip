@@ -29,7 +29,8 @@
 #define MPLC_WSPEC 1  // conv_wgrad: the sample loop compiled per wave (compile-time transform signs)
 #endif
 #ifndef MPLC_WSPEC_FWD
-#define MPLC_WSPEC_FWD 1  // conv_fwd likewise
+#define MPLC_WSPEC_FWD 0  // conv_fwd likewise: -1.5 % on the probe, but 19 registers spill and at the bench's size the
+                          // kernel ran +2.2 % with 6 % more HBM traffic (the scratch), profiles/r04_pmc_traffic_v3.json
 #endif
 template <int V>
 struct IntC {
