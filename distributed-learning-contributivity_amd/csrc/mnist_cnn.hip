@@ -26,11 +26,9 @@
 #include "xcd.h"
 
 #ifndef MPLC_WSPEC
-#define MPLC_WSPEC 1  // conv_wgrad: the sample loop compiled per wave (compile-time transform signs)
-#endif
-#ifndef MPLC_WSPEC_FWD
-#define MPLC_WSPEC_FWD 0  // conv_fwd likewise: -1.5 % on the probe, but 19 registers spill and at the bench's size the
-                          // kernel ran +2.2 % with 6 % more HBM traffic (the scratch), profiles/r04_pmc_traffic_v3.json
+#define MPLC_WSPEC 1  // conv_wgrad: the sample loop compiled per wave (compile-time transform signs).  conv_fwd in
+                      // the same form: -1.5 % on the probe, but 19 registers spill and at the bench's size it ran
+                      // +2.2 % with 6 % more HBM traffic (scratch), profiles/r04_pmc_traffic_v3.json: not kept
 #endif
 template <int V>
 struct IntC {
@@ -301,6 +299,11 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
   // B^T row i combines input rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
+  const int ra = (wi == 0) ? 0 : 1;
+  const int rb = (wi == 3) ? 3 : 2;
+  const float sa = (wi == 2) ? -1.0f : 1.0f;
+  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
+  const int drow = (rb - ra) * A1 * A1P;
   // the wave's B operands of all 8 k-steps (its transform row of U), resident for the whole block
   const float* Ub = U + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C1 * C2 + kq * C2 + tl;
   const float bias = P[OFF_B2 + (tid & 63)];  // the output phase's channel co = tid & 63 in every pass
@@ -319,16 +322,6 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   store_img(img_s[0]);
   if (j_begin + 1 < j_end) load_img(j_begin + 1);  // in flight during the first sample
   __syncthreads();
-  // the sample loop compiled once per wave (MPLC_WSPEC): the wave's transform row i fixes B^T's signs, so V takes
-  // one add / subtract per value instead of a multiply and a multiply-add (products by +-1 are exact: same values)
-  auto samples = [&](auto wtag) __attribute__((always_inline)) {
-  constexpr int WIC = decltype(wtag)::value;
-  const int wv = WIC >= 0 ? WIC : wi;
-  const int ra = (wv == 0) ? 0 : 1;
-  const int rb = (wv == 3) ? 3 : 2;
-  const float sa = (wv == 2) ? -1.0f : 1.0f;
-  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
-  const int drow = (rb - ra) * A1 * A1P;
 #pragma unroll 1
   for (int j = j_begin; j < j_end; ++j) {
     // a1_s is free (the previous sample's last two barriers follow its last GEMM read); this sample's image is
@@ -381,12 +374,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       auto make_v = [&](float (&v)[4]) {
         float t[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if constexpr (WIC >= 0)
-            t[c] = (WIC == 2 ? -pn[c] : pn[c]) + (WIC == 0 || WIC == 3 ? -pn[4 + c] : pn[4 + c]);
-          else
-            t[c] = sa * pn[c] + sb * pn[4 + c];
-        }
+        for (int c = 0; c < 4; ++c) t[c] = sa * pn[c] + sb * pn[4 + c];
         v[0] = t[0] - t[2];
         v[1] = t[1] + t[2];
         v[2] = t[2] - t[1];
@@ -454,17 +442,6 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       }
       __syncthreads();
     }
-  }
-  };
-  if constexpr (MPLC_WSPEC_FWD) {
-    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
-      case 0: samples(IntC<0>{}); break;
-      case 1: samples(IntC<1>{}); break;
-      case 2: samples(IntC<2>{}); break;
-      default: samples(IntC<3>{}); break;
-    }
-  } else {
-    samples(IntC<-1>{});
   }
 }
 
