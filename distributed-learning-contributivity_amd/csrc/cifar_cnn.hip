@@ -476,31 +476,42 @@ __device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
 // value at its argmax pixel, 0 at the other three and outside the pooled grid (an odd dense size's last row / column
 // belongs to no window).  Window-major: one (window, channel quad) per item, so one 16-B value load and one 4-B code
 // load feed 4 pixels.  The LDS image is exactly what the dense un-pooled tensor held.
-template <int HP, int WP, int C, int NR, int NC, int CP, int NTHR>
-__device__ __forceinline__ void stage_unpool(const float* __restrict__ pooled, const uint8_t* __restrict__ codes,
-                                             int iy0, int ix0, float* __restrict__ dst, int tid) {
-  constexpr int C4 = C / 4;
-  constexpr int TOT = (NR / 2) * (NC / 2) * C4;
-  constexpr int NIT = (TOT + NTHR - 1) / NTHR;
-  fvec4 val[NIT];
-  uint32_t cw[NIT];
+template <int C, int NR, int NC, int NTHR>
+struct UnpoolShape {
+  static constexpr int C4 = C / 4;
+  static constexpr int TOT = (NR / 2) * (NC / 2) * C4;
+  static constexpr int NIT = (TOT + NTHR - 1) / NTHR;
+};
+// the two halves of stage_unpool: the loads into registers (val, cw), then the LDS image from them
+template <int HP, int WP, int C, int NR, int NC, int NTHR>
+__device__ __forceinline__ void unpool_load(const float* __restrict__ pooled, const uint8_t* __restrict__ codes,
+                                            int iy0, int ix0, int tid,
+                                            fvec4 (&val)[UnpoolShape<C, NR, NC, NTHR>::NIT],
+                                            uint32_t (&cw)[UnpoolShape<C, NR, NC, NTHR>::NIT]) {
+  using S = UnpoolShape<C, NR, NC, NTHR>;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < S::NIT; ++k) {
     const int e = tid + k * NTHR;
-    const int win = e / C4, c4 = e % C4;
+    const int win = e / S::C4, c4 = e % S::C4;
     const int py = iy0 / 2 + win / (NC / 2), px = ix0 / 2 + win % (NC / 2);
-    const bool ok = e < TOT && py >= 0 && py < HP && px >= 0 && px < WP;
+    const bool ok = e < S::TOT && py >= 0 && py < HP && px >= 0 && px < WP;
     const int pidx = (py * WP + px) * C + 4 * c4;
     const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? pooled + pidx : pooled);
     const uint32_t c = *reinterpret_cast<const uint32_t*>(ok ? codes + pidx : codes);
     val[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
     cw[k] = c;
   }
+}
+template <int C, int NR, int NC, int CP, int NTHR>
+__device__ __forceinline__ void unpool_store(float* __restrict__ dst, int tid,
+                                             const fvec4 (&val)[UnpoolShape<C, NR, NC, NTHR>::NIT],
+                                             const uint32_t (&cw)[UnpoolShape<C, NR, NC, NTHR>::NIT]) {
+  using S = UnpoolShape<C, NR, NC, NTHR>;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < S::NIT; ++k) {
     const int e = tid + k * NTHR;
-    if (e < TOT) {
-      const int win = e / C4, c4 = e % C4;
+    if (e < S::TOT) {
+      const int win = e / S::C4, c4 = e % S::C4;
       float* d0 = dst + ((2 * (win / (NC / 2))) * NC + 2 * (win % (NC / 2))) * CP + 4 * c4;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -512,6 +523,15 @@ __device__ __forceinline__ void stage_unpool(const float* __restrict__ pooled, c
       }
     }
   }
+}
+template <int HP, int WP, int C, int NR, int NC, int CP, int NTHR>
+__device__ __forceinline__ void stage_unpool(const float* __restrict__ pooled, const uint8_t* __restrict__ codes,
+                                             int iy0, int ix0, float* __restrict__ dst, int tid) {
+  using S = UnpoolShape<C, NR, NC, NTHR>;
+  fvec4 val[S::NIT];
+  uint32_t cw[S::NIT];
+  unpool_load<HP, WP, C, NR, NC, NTHR>(pooled, codes, iy0, ix0, tid, val, cw);
+  unpool_store<C, NR, NC, CP, NTHR>(dst, tid, val, cw);
 }
 
 __device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) {  // o = G g (one column)
@@ -636,6 +656,12 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
+#ifndef MPLC_WG_PIPE
+#define MPLC_WG_PIPE 1  // conv2's weight gradient: the next band's staging loads in flight during this band's MFMAs
+#endif
+#ifndef MPLC_WG_PIPE4
+#define MPLC_WG_PIPE4 1  // conv4's weight gradient likewise (conv3's would spill 24 registers: not pipelined)
+#endif
 #ifndef MPLC_ROW_WSPEC
 #define MPLC_ROW_WSPEC 1  // wino_kernel: the group loop compiled per wave (compile-time B^T signs)
 #endif
@@ -1394,7 +1420,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // fold their row of the inverse transform (P_i = M_i G) and exchange it through LDS, 16 input channels at a
 // time.  Samples, bands and tiles in a fixed order: sums independent of which replicas share the launch.
 // ------------------------------------------------------------------------------------------------
-template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BTY, int CIB, int UPZ = 0>
+template <int HI, int WI, int CI, int CO, int PAD, int HOV, int WOV, int BTY, int CIB, int UPZ = 0, int PIPE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wgrad_kernel(const WgArgs a) {
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr int TY = (HOV + 1) / 2, TX = (WOV + 1) / 2;
@@ -1441,72 +1467,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float ai0 = (wv == 3) ? 0.0f : 1.0f;                       // A[i][0]
   const float ai1 = (wv == 0) ? 0.0f : ((wv == 1) ? 1.0f : -1.0f);  // A[i][1]
   const int drow = (rb - ra) * XROW;
+  // staging of (sample, band) in two halves: the global loads into registers, then the LDS images.  PIPE: the
+  // next band's loads are issued right after this band's LDS stores, so that they land during this band's MFMAs
+  // (the same values in the same places: bit-identical); otherwise loads and stores back to back.
+  constexpr int C4X = CIB / 4;
+  constexpr int TOTX = LR * LC * C4X;
+  constexpr int NITX = (TOTX + 255) / 256;
+  using ZU = UnpoolShape<CO, ZR, ZC, 256>;
+  constexpr int Z4 = CO / 4;
+  constexpr int TOTZ = ZR * ZC * Z4;
+  constexpr int NITZ = UPZ ? ZU::NIT : (TOTZ + 255) / 256;
+  static_assert(UPZ || 256 % Z4 == 0, "db needs a fixed channel quad per thread");
+  static_assert(!UPZ || (ZR % 2 == 0 && ZC % 2 == 0 && HOV == 2 * (HO / 2) && WOV == 2 * (WO / 2)), "whole windows");
+  fvec4 xv[NITX], zv[NITZ];
+  uint32_t zc[UPZ ? NITZ : 1];
+  auto stage_load = [&](int jj, int bnd) {
+    const int64_t sl = (int64_t)r * a.bmax + jj;
+    const float* X = a.x + sl * (HI * WI * CI) + chn * CIB;
+    const float* Z = a.dz + sl * (HO * WO * CO);
+    const int ty0 = bnd * BTY;
+#pragma unroll
+    for (int k = 0; k < NITX; ++k) {  // input rows 2 ty0 - PAD .., columns -PAD .., the chunk's channels
+      const int e4 = tid + k * 256;
+      const int pix = e4 / C4X, c4 = e4 % C4X;
+      const int iy = 2 * ty0 - PAD + pix / LC, ix = pix % LC - PAD;
+      const bool ok = e4 < TOTX && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+      const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? X + (iy * WI + ix) * CI + 4 * c4 : X);
+      xv[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    if constexpr (UPZ) {  // pooled dZ [HO/2][WO/2][CO] with its codes, un-pooled window-major
+      unpool_load<HO / 2, WO / 2, CO, ZR, ZC, 256>(Z, a.dz_code + sl * ((HO / 2) * (WO / 2) * CO), 2 * ty0, 0, tid,
+                                                  zv, zc);
+    } else {  // dZ rows 2 ty0 .. (zero beyond HOV x WOV)
+#pragma unroll
+      for (int k = 0; k < NITZ; ++k) {
+        const int e4 = tid + k * 256;
+        const int pix = e4 / Z4, c4 = e4 % Z4;
+        const int yy = 2 * ty0 + pix / ZC, xx = pix % ZC;
+        const bool ok = e4 < TOTZ && yy < HOV && xx < WOV;
+        const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? Z + (yy * WO + xx) * CO + 4 * c4 : Z);
+        zv[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    }
+  };
+  auto stage_store = [&]() {
+#pragma unroll
+    for (int k = 0; k < NITX; ++k) {
+      const int e4 = tid + k * 256;
+      if (e4 < TOTX) {
+        float* d = x_s + (e4 / C4X) * CIP + 4 * (e4 % C4X);
+        d[0] = xv[k].x;
+        d[1] = xv[k].y;
+        d[2] = xv[k].z;
+        d[3] = xv[k].w;
+      }
+    }
+    if constexpr (UPZ) {
+      unpool_store<CO, ZR, ZC, COP, 256>(z_s, tid, zv, zc);  // db below, from the staged image
+    } else {
+#pragma unroll
+      for (int k = 0; k < NITZ; ++k) {
+        const int e4 = tid + k * 256;
+        if (e4 < TOTZ) {
+          float* d = z_s + (e4 / Z4) * COP + 4 * (e4 % Z4);
+          d[0] = zv[k].x;
+          d[1] = zv[k].y;
+          d[2] = zv[k].z;
+          d[3] = zv[k].w;
+          gb += zv[k];  // db from the same values (chunk 0 only); rows beyond HOV / WOV hold 0
+        }
+      }
+    }
+  };
+  if constexpr (PIPE) stage_load(j_begin, 0);
   for (int j = j_begin; j < j_end; ++j) {
-    const int64_t slot = (int64_t)r * a.bmax + j;
-    const float* X = a.x + slot * (HI * WI * CI) + chn * CIB;
-    const float* Z = a.dz + slot * (HO * WO * CO);
 #pragma unroll 1
     for (int band = 0; band < NB; ++band) {
       const int ty0 = band * BTY;
       const int bty = min(BTY, TY - ty0);
       __syncthreads();  // the previous band's readers are done
-      {  // input rows 2 ty0 - PAD .., columns -PAD .., this chunk's channels (zero outside the input)
-        constexpr int C4 = CIB / 4;
-        constexpr int TOT = LR * LC * C4;
-        constexpr int NIT = (TOT + 255) / 256;
-        fvec4 v[NIT];
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-          const int e4 = tid + k * 256;
-          const int pix = e4 / C4, c4 = e4 % C4;
-          const int iy = 2 * ty0 - PAD + pix / LC, ix = pix % LC - PAD;
-          const bool ok = e4 < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
-          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? X + (iy * WI + ix) * CI + 4 * c4 : X);
-          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-          const int e4 = tid + k * 256;
-          if (e4 < TOT) {
-            float* d = x_s + (e4 / C4) * CIP + 4 * (e4 % C4);
-            d[0] = v[k].x;
-            d[1] = v[k].y;
-            d[2] = v[k].z;
-            d[3] = v[k].w;
-          }
-        }
-      }
-      if constexpr (UPZ) {  // pooled dZ [HO/2][WO/2][CO] with its codes, un-pooled window-major; db below
-        static_assert(ZR % 2 == 0 && ZC % 2 == 0 && HOV == 2 * (HO / 2) && WOV == 2 * (WO / 2), "whole windows");
-        stage_unpool<HO / 2, WO / 2, CO, ZR, ZC, COP, 256>(Z, a.dz_code + slot * ((HO / 2) * (WO / 2) * CO), 2 * ty0,
-                                                           0, z_s, tid);
-      } else {  // dZ rows 2 ty0 .. (zero beyond HOV x WOV); db from the same loads (chunk 0 only)
-        constexpr int Z4 = CO / 4;
-        constexpr int TOT = ZR * ZC * Z4;
-        constexpr int NIT = (TOT + 255) / 256;
-        static_assert(256 % Z4 == 0, "db needs a fixed channel quad per thread");
-        fvec4 v[NIT];
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-          const int e4 = tid + k * 256;
-          const int pix = e4 / Z4, c4 = e4 % Z4;
-          const int yy = 2 * ty0 + pix / ZC, xx = pix % ZC;
-          const bool ok = e4 < TOT && yy < HOV && xx < WOV;
-          const fvec4 t = *reinterpret_cast<const fvec4*>(ok ? Z + (yy * WO + xx) * CO + 4 * c4 : Z);
-          v[k] = ok ? t : fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) {
-          const int e4 = tid + k * 256;
-          if (e4 < TOT) {
-            float* d = z_s + (e4 / Z4) * COP + 4 * (e4 % Z4);
-            d[0] = v[k].x;
-            d[1] = v[k].y;
-            d[2] = v[k].z;
-            d[3] = v[k].w;
-            gb += v[k];  // rows beyond HOV / WOV load 0
-          }
-        }
+      if constexpr (!PIPE) stage_load(j, band);
+      stage_store();
+      if constexpr (PIPE) {  // the next band (or the next sample's first) in flight during this band's MFMAs
+        const bool last = band + 1 == NB;
+        if (!last || j + 1 < j_end) stage_load(last ? j + 1 : j, last ? 0 : band + 1);
       }
       __syncthreads();
       if constexpr (UPZ) {  // db from the staged image, summed in the dense staging's order (bit-identical)
@@ -2268,9 +2312,9 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK, 1>   /* 8x8 tiles,    2 bands, 63.7 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 // Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
-#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1>  /* 15x15 tiles, 5 bands, 56.9 KB */
+#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1, MPLC_WG_PIPE>  /* 15x15 tiles, 5 bands, 56.9 KB */
 #define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 57.1 KB */
-#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1>  /* 6x6 tiles, 1 band, 2 ci chunks */
+#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1, MPLC_WG_PIPE4>  /* 6x6 tiles, 1 band, 2 ci chunks */
 
 inline int launch_status() {
   const hipError_t e = hipGetLastError();
