@@ -657,10 +657,11 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
 }
 
 #ifndef MPLC_WG_PIPE
-#define MPLC_WG_PIPE 1  // conv2's weight gradient: the next band's staging loads in flight during this band's MFMAs
+#define MPLC_WG_PIPE 0  // conv2's weight gradient: the next band's staging loads in flight during this band's MFMAs
+                        // (measured 115 vs 113-114 ms for the split staging without it: off)
 #endif
 #ifndef MPLC_WG_PIPE4
-#define MPLC_WG_PIPE4 1  // conv4's weight gradient likewise (conv3's would spill 24 registers: not pipelined)
+#define MPLC_WG_PIPE4 1  // conv4's weight gradient likewise: -2 % (conv3's would spill 24 registers: not pipelined)
 #endif
 #ifndef MPLC_ROW_WSPEC
 #define MPLC_ROW_WSPEC 1  // wino_kernel: the group loop compiled per wave (compile-time B^T signs)
