@@ -2079,6 +2079,7 @@ constexpr int D5M_DHS = HID + 20;       // dh row stride: conflict-free dd4 oper
 constexpr int D5M_XS = 128 + 4;         // transpose scratch row stride (a wave's 128 columns)
 constexpr int D5M_STAGE = D5M_SCHUNK * D5M_DHS;
 constexpr int D5M_LDS = (D5M_STAGE > 4 * 16 * D5M_XS) ? D5M_STAGE : 4 * 16 * D5M_XS;
+static_assert(HID == 512 && FEAT % D5M_ROWS == 0, "dense5_bwd_kernel: 4 waves x 128 columns, 16-row slices");
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense5_bwd_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,

@@ -833,6 +833,7 @@ constexpr int D1M_PS = D1M_ROWS + 16;  // p row stride
 constexpr int D1M_XS = HID + 4;  // transpose scratch row stride (4 tl + kq: conflict-free)
 constexpr int D1M_STAGE = D1M_SCHUNK * (D1M_DHS + D1M_PS);
 constexpr int D1M_LDS = (D1M_STAGE > 4 * 16 * D1M_XS) ? D1M_STAGE : 4 * 16 * D1M_XS;
+static_assert(HID == 128 && FEAT % D1M_ROWS == 0, "dense1_bwd_adam_mfma_kernel: 8 column tiles, 64-row slices");
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dense1_bwd_adam_mfma_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
