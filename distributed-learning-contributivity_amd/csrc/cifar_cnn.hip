@@ -1710,7 +1710,12 @@ __global__ void rmsprop_small_kernel(const int32_t* __restrict__ cnt, const int3
 // Dense(512) + ReLU (+ dropout .5 when training): H[slot][n] = relu(sum_k D4[slot][k] W5[k][n] + b5[n]).
 // Block = 32 samples x 128 columns (4 waves x 32); A staged in LDS, W5 streamed.
 // ------------------------------------------------------------------------------------------------
-constexpr int DF_K = 64;
+#ifndef MPLC_D5F_K
+#define MPLC_D5F_K 32  // dense5_fwd: rows of W5 per K chunk (the MFMA chain order is the same for any): 32 -2 % vs 64
+                       // (76 registers, more waves); 128 / 192 +6 % / +30 % (219 / 256 registers)
+#endif
+constexpr int DF_K = MPLC_D5F_K;
+static_assert(FEAT % DF_K == 0, "dense5_fwd K chunks");
 
 __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict__ A, const int32_t* __restrict__ cnt,
                                                          int cnt_all, int bmax, const float* __restrict__ params,
