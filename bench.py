@@ -1,6 +1,6 @@
 """Benchmark driver (contract: one JSON line on rank 0).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--leg train|shapley|cifar] [--budget-s B]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--leg train|shapley|cifar|titanic] [--budget-s B]
 
 leg "train" (default; BASELINE.json metric "coalition v(S) evals/sec (MNIST FedAvg)"): BASELINE config #3
   - MNIST CNN, 10 partners, random split ([0.1]*10), FedAvg, exact "Shapley values" over all 1023
@@ -13,6 +13,9 @@ leg "train" (default; BASELINE.json metric "coalition v(S) evals/sec (MNIST FedA
   the job is fixed).
   Also reported: "shapley_agg" - the exact-Shapley aggregation kernel on a 2^28 fp64 table (config #5).
 leg "shapley": only the N=28 aggregation (GB/s).
+leg "titanic" (BASELINE config #2): Titanic-shaped data, 10 partners, FedAvg logistic regression (E=3, M=1), exact
+  "Shapley values" over all 1023 coalitions; value = coalitions / second.  Also the "config2" sub-object of the
+  default line, beside the oracle's single-thread rate and the reference's own measured 10.1 evals/s.
 leg "cifar" (BASELINE config #4): CIFAR10 CNN, 20 partners, FedAvg, "TMCS" (default; --method SMCS etc.) with
   the reference's defaults (sv_accuracy .01, alpha .95, truncation .05), fixed E=1, M=20, G=8.  CIFAR10-shaped
   synthetic data with class templates (signal 0.4: accuracy grows with the data a coalition holds, so the
@@ -517,8 +520,10 @@ def bench_train(args, rank, world):
     # reserve: the N=28 aggregation leg (~10 s with its table), at N=1 the bounded CPU baselines (~40 s + ~15 s)
     # and the config #4 sub-leg (one CIFAR10 TMCS run: ~110 s on one GPU)
     # (measured on the box, round 3: aggregation 1.3 s, CPU baselines 13 s + 6 s, the CIFAR run 107 s)
+    # and the config #2 sub-leg (Titanic: a warm-up and a few sub-second sweeps, its CPU baseline 10 s)
     reserve = ((0 if args.no_shapley_agg else 10) + (25 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
-               + (0 if args.no_cifar else CIFAR_SUBLEG_S / world + 15 + (15 if world == 1 else 0)))
+               + (0 if args.no_cifar else CIFAR_SUBLEG_S / world + 15 + (15 if world == 1 else 0))
+               + (0 if args.no_titanic else 15 + (12 if world == 1 and not args.no_cpu_baseline else 0)))
     steps, warm, wall, c, per_step = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
@@ -814,6 +819,86 @@ def bench_cifar(args, rank, world, sub=False):
     return out, sc, coals
 
 
+# --------------------------------------------------------------------------------------------------
+# Titanic leg (config #2)
+# --------------------------------------------------------------------------------------------------
+REFERENCE_TITANIC_EVALS_S = 10.1  # BASELINE.md / SURVEY 6: the reference's FedAvg + sklearn LR, measured in the build
+                                  # container (60 random coalitions |S| >= 2, one CPU thread); not a published number
+
+
+def build_titanic_scenario(partners=10, epochs=3, M=1):
+    from mplc.dataset import Titanic
+    from mplc.scenario import Scenario
+    return Scenario(partners, [1.0 / partners] * partners if partners != 10 else [0.1] * 10,
+                    dataset=Titanic(synthetic=True), epoch_count=epochs, minibatch_count=M,
+                    is_early_stopping=False).provision()
+
+
+def cpu_baseline_titanic(sc, coalitions, epochs, max_s=10.0):
+    """The oracle (oracle/lr.py: every partner fit solved exactly by float64 Newton, the reference's sequential
+    FedAvg: each of the E rounds refits every partner, np.average with data-volume weights, test accuracy) on one
+    host thread, coalitions in a fixed shuffled order until max_s seconds: evals/s of that sample."""
+    import numpy as np
+    from oracle import lr as olr
+    parts = [(np.asarray(p.x_train, dtype=np.float64), np.asarray(p.y_train)) for p in sc.partners_list]
+    xte, yte = np.asarray(sc.dataset.x_test, dtype=np.float64), np.asarray(sc.dataset.y_test)
+    order = np.random.default_rng(0).permutation(len(coalitions))
+    done, t0 = 0, time.perf_counter()
+    for i in order:
+        coal = coalitions[i]
+        sizes = [len(parts[p][1]) for p in coal]
+        for _ in range(epochs):  # the M=1 rounds: every partner refits (warm start, same optimum) then the average
+            thetas = [olr.fit_exact(*parts[p]) for p in coal]
+            theta = np.average(np.array(thetas), axis=0, weights=np.asarray(sizes) / np.sum(sizes))
+        olr.accuracy(theta, xte, yte)
+        done += 1
+        if time.perf_counter() - t0 > max_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 3), "unit": "coalition evals/s", "cores": 1, "kind": "port",
+            "sample": f"{done} of the {len(coalitions)} coalitions (fixed shuffled order), oracle/lr.py exact fits, "
+                      f"E={epochs} rounds each, {dt:.1f}s",
+            "reference_measured": {"value": REFERENCE_TITANIC_EVALS_S, "unit": "coalition evals/s", "cores": 1,
+                                   "note": "the reference's own FedAvg orchestration with sklearn lbfgs LR on this "
+                                           "shape, 60 random coalitions |S| >= 2, timed in the build container "
+                                           "(BASELINE.md, SURVEY 6)"}}
+
+
+def bench_titanic(args, rank, world, sub=False):
+    """Config #2: Titanic-shaped data, 10 partners, FedAvg logistic regression (E=3, M=1 as the reference's e2e
+    test), exact "Shapley values" over all 1023 coalitions; one step = one full compute_contributivity (a fresh
+    coalition cache each time).  Every coalition's whole FedAvg runs in one workgroup of one launch
+    (csrc/logreg.hip), so the step is launch- and latency-bound, not a roofline kernel."""
+    import torch
+    from mplc.contributivity import Contributivity
+    from mplc.engine import CoalitionEngine
+    sc = build_titanic_scenario(10, 3, 1)
+    sc.engine = CoalitionEngine.for_scenario(sc)
+
+    def one_step():
+        sc.coalition_values = {}
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity("Shapley values")
+        torch.cuda.synchronize()
+        return c
+
+    steps_max = 10 if sub else None
+    steps, warm, wall, c, per_step = run_budgeted(one_step, lambda i, n: one_step(), args, world, 0, "titanic",
+                                                  max_steps=steps_max, warmup=1)
+    coals = [k for k in c.charac_fct_values if len(k)]
+    out = {"metric": "coalition v(S) evals/sec (Titanic FedAvg LR, exact Shapley)",
+           "value": round(c.first_charac_fct_calls_count * steps / wall, 2), "unit": "coalition evals/s",
+           "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": round(wall * 1000 / steps, 2),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (Titanic-shaped: sklearn make_classification(887, 27, n_informative=8, random_state=0))",
+           "config": {"workload": "BASELINE config #2: Titanic-shaped, 10 partners x 0.1, FedAvg logistic regression "
+                                  f"(E=3, M=1), exact Shapley over all 1023 coalitions, coalitions LPT-sharded x{world}",
+                      "coalitions_evaluated": c.first_charac_fct_calls_count,
+                      "shapley": [round(float(v), 6) for v in c.contributivity_scores],
+                      "per_step_ms": [round(t * 1000, 2) for t in per_step]}}
+    return out, sc, coals
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -821,7 +906,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--budget-s", type=float, default=480.0,
                     help="wall-clock budget from process start for the whole run (driver limit: 600 s)")
-    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar", "dist-check"])
+    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar", "titanic", "dist-check"])
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
     ap.add_argument("--cifar-epochs", type=int, default=1)
@@ -835,6 +920,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shapley-agg", action="store_true")
     ap.add_argument("--no-cifar", action="store_true", help="leave out the config #4 sub-leg of the default line")
+    ap.add_argument("--no-titanic", action="store_true", help="leave out the config #2 sub-leg of the default line")
     ap.add_argument("--early-stopping", action="store_true",
                     help="train leg at the reference's stopping rule (with --epochs 40: its defaults)")
     ap.add_argument("--mnist-signal", type=float, default=0.0,
@@ -882,6 +968,10 @@ def main():
                                                                 f"range-sharded + RCCL all-reduce x{world}"}})
         if rank == 0:
             out["cpu_baseline"] = cpu_baseline_shapley() if (world == 1 and not args.no_cpu_baseline) else None
+    elif args.leg == "titanic":
+        out, sc, coals = bench_titanic(args, rank, world)
+        if rank == 0:
+            out["cpu_baseline"] = cpu_baseline_titanic(sc, coals, 3) if (world == 1 and not args.no_cpu_baseline) else None
     elif args.leg == "cifar":
         out, sc, coals = bench_cifar(args, rank, world)
         if rank == 0:
@@ -917,6 +1007,16 @@ def main():
                 c4.pop(k, None)
             out["config4"] = c4
             log(f"config #4 sub-leg: {c4['value']} evals/s")
+        if not args.no_titanic:
+            # BASELINE config #2 in the same line: the Titanic LR exact-Shapley sweep (a few seconds)
+            c2, c2_sc, c2_coals = bench_titanic(args, rank, world, sub=True)
+            if rank == 0:
+                c2["cpu_baseline"] = (cpu_baseline_titanic(c2_sc, c2_coals, 3)
+                                      if (world == 1 and not args.no_cpu_baseline) else None)
+            for k in ("n_gpus", "higher_is_better", "scaling", "vs_baseline", "budget"):
+                c2.pop(k, None)
+            out["config2"] = c2
+            log(f"config #2 sub-leg: {c2['value']} evals/s")
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
                                    if (world == 1 and not args.no_cpu_baseline) else None)

@@ -41,7 +41,7 @@ def _stale(target, deps):
 # shuffles that feed it) issued beside f32 MFMAs costs more issue cycles than the scalar ops it replaces
 # (MI355X_MICROARCH.md, per-instruction cycle constants), and it hoisted the Winograd V arithmetic of the
 # software-pipelined conv k-loops out of the MFMA gaps.
-FILE_FLAGS = {"mnist_cnn.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"mnist_cnn.hip": ["-fno-slp-vectorize"], "mnist_wgrad.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src, obj, verbose):

@@ -2261,40 +2261,54 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
   const float* P = params + (int64_t)mdl * stride;
   for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
   __syncthreads();
-  double lsum = 0.0;
+  // The loss is summed in fixed blocks of 256 samples (the tree below), added to the model's running total in
+  // block order: with every chunk but the last a multiple of 256 samples (the host's rule), the total is the same
+  // bits whatever the chunk size - and the chunk size depends on how many models share the evaluation.
+  double run = (tid == 0) ? loss_sum[mdl] : 0.0;
   int csum = 0;
-  for (int jj = tid; jj < count; jj += 256) {
-    const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
-    float z[NCLS];
+  for (int b0 = 0; b0 < count; b0 += 256) {
+    const int jj = b0 + tid;
+    double lv = 0.0;
+    if (jj < count) {
+      const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
+      float z[NCLS];
 #pragma unroll
-    for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
-    for (int c = 0; c < HID; ++c) {
-      const float hv = h[c];
+      for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
+      for (int c = 0; c < HID; ++c) {
+        const float hv = h[c];
 #pragma unroll
-      for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
+        for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
+      }
+      int am = 0;
+      float mx = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o)
+        if (z[o] > mx) { mx = z[o]; am = o; }
+      float s = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
+      const int y = labels[row_base + jj];
+      lv = (double)(logf(s) + mx - z[y]);
+      csum += (am == y) ? 1 : 0;
     }
-    int am = 0;
-    float mx = z[0];
-#pragma unroll
-    for (int o = 1; o < NCLS; ++o)
-      if (z[o] > mx) { mx = z[o]; am = o; }
-    float s = 0.0f;
-#pragma unroll
-    for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
-    const int y = labels[row_base + jj];
-    lsum += (double)(logf(s) + mx - z[y]);
-    csum += (am == y) ? 1 : 0;
+    ls[tid] = lv;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+      if (tid < off) ls[tid] += ls[tid + off];
+      __syncthreads();
+    }
+    if (tid == 0) run += ls[0];
+    __syncthreads();  // ls is rewritten by the next block
   }
-  ls[tid] = lsum;
   cs[tid] = csum;
   __syncthreads();
   for (int off = 128; off >= 1; off >>= 1) {
-    if (tid < off) { ls[tid] += ls[tid + off]; cs[tid] += cs[tid + off]; }
+    if (tid < off) cs[tid] += cs[tid + off];
     __syncthreads();
   }
   if (tid == 0) {
     correct[mdl] += cs[0];
-    loss_sum[mdl] += ls[0];
+    loss_sum[mdl] = run;
   }
 }
 

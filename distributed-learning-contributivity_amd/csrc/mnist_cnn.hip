@@ -19,108 +19,9 @@
 // Everything is fp32 (the reference's Keras float32), accumulation on the exact-f32 MFMA.
 // conv1's output (86.5 KB/sample) is never written to HBM: it is recomputed (9 MACs/element) by the
 // three kernels that need it.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include "mplc_hip.h"
-#include "keyed.h"
-#include "xcd.h"
-
-#ifndef MPLC_WSPEC
-#define MPLC_WSPEC 1  // conv_wgrad: the sample loop compiled per wave (compile-time transform signs).  conv_fwd in
-                      // the same form: -1.5 % on the probe, but 19 registers spill and at the bench's size it ran
-                      // +2.2 % with 6 % more HBM traffic (scratch), profiles/r04_pmc_traffic_v3.json: not kept
-#endif
-template <int V>
-struct IntC {
-  static constexpr int value = V;
-};
-
-// Timing-experiment switches compile parts of a kernel out and give WRONG results by design (A/B probes of
-// where a kernel's time goes).  A product build must never carry one.
-#if (defined(BWD_EXP_NOSTAGE) || defined(BWD_EXP_NOSTAGE_UR) || defined(BWD_EXP_NOSTAGE_DZ) || \
-     defined(BWD_EXP_NOEPI) || defined(WG_EXP_NOCONV1) || defined(WG_EXP_NOGEMM)) && !defined(MPLC_EXPERIMENT)
-#error "a *_EXP_* timing switch produces wrong results: define MPLC_EXPERIMENT for an A/B experiment build"
-#endif
+#include "mnist_common.h"
 
 namespace {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float fvec4 __attribute__((ext_vector_type(4)));
-typedef float fvec2 __attribute__((ext_vector_type(2)));
-
-constexpr int IMG = 28;
-constexpr int A1 = 26;
-constexpr int C1 = 32;
-constexpr int Z2 = 24;
-constexpr int C2 = 64;
-constexpr int PL = 12;
-constexpr int FEAT = 9216;
-constexpr int HID = 128;
-constexpr int NCLS = 10;
-constexpr int64_t OFF_W1 = MPLC_CNN_OFF_W1, OFF_B1 = MPLC_CNN_OFF_B1, OFF_W2 = MPLC_CNN_OFF_W2,
-                  OFF_B2 = MPLC_CNN_OFF_B2, OFF_W3 = MPLC_CNN_OFF_W3, OFF_B3 = MPLC_CNN_OFF_B3,
-                  OFF_W4 = MPLC_CNN_OFF_W4, OFF_B4 = MPLC_CNN_OFF_B4;
-constexpr int ADAM_LAST = 1 << 30;  // adam_t flag: the optimizer's last step
-constexpr int A1P = 33;  // padded channel stride of conv1 output tiles in LDS (bank-conflict-free A reads)
-
-// Register cap of the three convolution kernels (build experiments: -DCONV_VGPR_CAP=N leaves 512 - 2N registers
-// per SIMD lane beside two convolution waves, room for a wave of another kernel)
-#ifdef CONV_VGPR_CAP
-#define CONV_REGS __attribute__((amdgpu_num_vgpr(CONV_VGPR_CAP)))
-#else
-#define CONV_REGS
-#endif
-
-// Cross-lane add within rows of 16 lanes on DPP (VALU, no LDS round trip).  Each level adds the partner's
-// value exactly as `d += __shfl_xor(d, m)` does (commutative adds of the same operands: bit-identical).
-template <int CTRL>
-__device__ __forceinline__ float dpp_partner(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
-constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
-constexpr int DPP_HALF_MIRROR = 0x141;  // lane i <-> 7 - i within 8 (the other quad after two levels)
-constexpr int DPP_MIRROR = 0x140;       // lane i <-> 15 - i within 16 (the other 8 after three levels)
-
-__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ floatx16 zero16() {
-  floatx16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.0f;
-  return z;
-}
-
-// conv1 weights as the MFMA B operand: lane (kh, ci) holds W1e[2s + kh][ci], s = 0..4, where W1e rows 0..8
-// are the 3x3 taps (ky*3 + kx) and row 9 is the bias.
-__device__ __forceinline__ void load_w1r(const float* __restrict__ P, int kh, int ci, float (&w1r)[5]) {
-#pragma unroll
-  for (int s = 0; s < 5; ++s) {
-    const int k = 2 * s + kh;
-    w1r[s] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : P[OFF_B1 + ci];
-  }
-}
-
-// conv1 + bias (pre-ReLU) of 32 positions on the fp32 MFMA: K = 9 taps + bias (patch value 1) in 5 k-steps.
-// Lane (kh, i) passes `pix`, the img_s offset of its position's top-left pixel (row stride IMG).
-// Result in accumulator layout: reg -> tile row (reg&3) + 8*(reg>>2) + 4*kh, column = channel lane&31.
-// All kernels that need conv1's output use this one routine, so forward and backward agree bit for bit.
-__device__ __forceinline__ floatx16 conv1_mfma(const float* img_s, int pix, int kh, const float (&w1r)[5]) {
-  floatx16 acc = zero16();
-  // tap k = 2s + kh at (k / 3) * IMG + k % 3
-  acc = mfma32(img_s[pix + (kh ? 1 : 0)], w1r[0], acc);
-  acc = mfma32(img_s[pix + (kh ? IMG : 2)], w1r[1], acc);
-  acc = mfma32(img_s[pix + (kh ? IMG + 2 : IMG + 1)], w1r[2], acc);
-  acc = mfma32(img_s[pix + (kh ? 2 * IMG + 1 : 2 * IMG)], w1r[3], acc);
-  const float a8 = img_s[pix + 2 * IMG + 2];
-  acc = mfma32(kh ? 1.0f : a8, w1r[4], acc);
-  return acc;
-}
-
-// accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
-__device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
 
 // ------------------------------------------------------------------------------------------------
 // Initialisation: glorot_uniform kernels (Keras default), zero biases / padding.
@@ -252,14 +153,7 @@ constexpr int FWD_TILES = FWD_PR * PL;             // 48 Winograd tiles (= pool 
 constexpr int FWD_TS = C2 + 1;                     // tile stride of a T plane (odd: conflict-free writes)
 constexpr int FWD_TQ = 16 * FWD_TS;                // one (row i, b) plane of T for a 16-tile group
 constexpr int FWD_NIT = (FWD_IMR * IMG + FWD_THREADS - 1) / FWD_THREADS;  // image values per thread
-#ifndef MPLC_FWD_SPB
-#define MPLC_FWD_SPB 9  // samples per block (config #3's bs 27 = 3 groups)
-#endif
-constexpr int FWD_SPB = MPLC_FWD_SPB;
-
-__device__ __forceinline__ fvec4 mfma16(float a, float b, fvec4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
+constexpr int FWD_SPB = 9;  // samples per block (config #3's bs 27 = 3 groups; 3: +1 %, 14 / 27: +1.2 % / +3 %)
 
 __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_fwd_kernel(
     const float* __restrict__ x, const int32_t* __restrict__ idx, int row_base, const int32_t* __restrict__ cnt,
@@ -676,9 +570,6 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 // Dense(128) backward + Adam, per 32-row slice of W3 (block = 256 threads: row = tid/8, 16 cols each)
 // dp[j][k] = sum_c dh[j][c] W3[k][c];  dW3[k][c] = sum_j p[j][k] dh[j][c];  db3 (slice 0 block)
 // ------------------------------------------------------------------------------------------------
-#ifndef MPLC_W1_LDS
-#define MPLC_W1_LDS 0  // conv_bwd_data / conv_wgrad read conv1's weights from an LDS copy (measured +0.5-0.9 %: off)
-#endif
 #ifndef MPLC_D1_MFMA
 #define MPLC_D1_MFMA 0  // dense1_bwd_adam_mfma_kernel (bit-identical MFMA form) instead of the VALU form: -4.7 % on the
                         // 1260-replica probe but +1.9 % at the bench's 5120 replicas (memory-bound there), so off
@@ -1072,10 +963,7 @@ constexpr int BWD_PAIRS = BWD_WR * PL * 16;    // (dp, code) pairs of a quarter
 constexpr int BWD_PRE = (BWD_PAIRS + BWD_THREADS - 1) / BWD_THREADS;
 constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quarter [co 16][ci 32][xi 16]
 constexpr int BWD_NIT = (IMG * IMG + BWD_THREADS - 1) / BWD_THREADS;  // image values per thread
-#ifndef MPLC_BWD_SPB
-#define MPLC_BWD_SPB 1  // samples per block (9: +2 % on the probe, the sample loop spills 13 registers)
-#endif
-constexpr int BWD_SPB = MPLC_BWD_SPB;
+constexpr int BWD_SPB = 1;  // samples per block (9: +2 % on the probe, the sample loop spills 13 registers)
 static_assert(BWD_BANDS * BWD_BAND_TILES >= BWD_TILES && (BWD_BANDS - 1) * BWD_BAND_TILES < BWD_TILES,
               "MPLC_CNN_W1_BANDS must be ceil(169 / 64)");
 
@@ -1087,7 +975,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   __shared__ fvec4 ur_s[BWD_UQ / 4];
   __shared__ float img_s[IMG * IMG];
   __shared__ float red_s[4][10 * 32];
-  __shared__ float w1_s[10 * C1];  // conv1's taps and bias (the epilogue's B operand), staged up front
   const int64_t lb = xcd_block();  // logical block (band, sample group, r), replica-major
   const int band = (int)(lb % BWD_BANDS);
   const int jg = (int)((lb / BWD_BANDS) % gridDim.y);
@@ -1132,10 +1019,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   };
   fetch(j_begin, 0);
   load_img(j_begin);
-  // conv1's weights for the epilogue: read here, where their latency hides behind the first quarter's staging,
-  // instead of from global memory at the epilogue's start (one exposed load round trip per block)
-  if (MPLC_W1_LDS)
-    for (int e = tid; e < 10 * C1; e += BWD_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
   {
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
@@ -1283,10 +1166,7 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = 4 * s3 + kq, ci = 16 * h + tl;
-      if (MPLC_W1_LDS)
-        w1b[s3][h] = (k < 10) ? w1_s[k * C1 + ci] : 0.0f;
-      else
-        w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
+      w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
     }
   fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
   fvec4 gacc1 = gacc;
@@ -1365,277 +1245,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   }  // samples
 }
 
-// ------------------------------------------------------------------------------------------------
-// conv2 weight gradient in Winograd form F(3x3, 2x2): per 2x2 tile of dZ2 (= one pooling window) and the
-// 4x4 conv1 patch it sees,  dW2[3x3] += G^T [ (A delta A^T) (.) (B^T d B) ] G  (the transposed dual of the
-// forward's F(2x2, 3x3); A, B, G are the forward's matrices).  The sum over tiles runs in the transformed
-// domain: 16 GEMMs M[xi][ci][co] = sum_tiles V[xi][tile][ci] D[xi][tile][co], then one inverse transform per
-// split: 2.25x fewer multiply-adds than the direct sum (16 per tile instead of 4 positions x 9 taps).
-// delta is the max-pool gradient of one window: a single nonzero v at the argmax (dy, dx) when positive,
-// so D = v * A[:, dy] (x) A[:, dx] is a sign pattern of v.
-// Block = (split s, replica r): samples [8s, 8s+8); 4 waves, wave i owns transform row i (xi = 4i .. 4i+3) x
-// 32 ci x 64 co (32 accumulators of v_mfma_f32_16x16x4_f32).  The work is a stream of bands (sample, 2 window
-// rows = 24 tiles): conv1 rows recomputed on MFMA (conv1_mfma, bit-identical to the forward's activations)
-// and the windows' (value, argmax) staged in LDS; per k-step of 4 tiles a lane forms 8 values of V (its
-// tile, two ci) and 16 of D (its tile, four co), for 32 MFMAs.  At the end the waves fold their row of the
-// inverse transform (P_i = M_i G) and exchange it through LDS.  Fixed-order sums: independent of which
-// other replicas share the launch.
-// ------------------------------------------------------------------------------------------------
-constexpr int WG_THREADS = 256;
-#ifndef MPLC_WG_SAMPLES
-#define MPLC_WG_SAMPLES 9  // bs 27 (config #3) = 3 equal splits: no short split block (8 -> 8, 8, 8, 3: +18 % wgrad)
-#endif
-constexpr int WG_SAMPLES = MPLC_WG_SAMPLES;       // samples per wgrad split (fixed: reproducible sums)
-constexpr int WG_PRE = 2 * PL * C2 / WG_THREADS;  // (dp, code) pairs per thread per band: 2 rows x 12 x 64
-// Staged operands are read as 8-byte pairs: a lane needs channels ci and 16 + ci of a conv1 position (stored
-// adjacent: slot 2 * (ci & 15) + (ci >> 4)) and (value, argmax) of a window channel (one int2), so a k-step's
-// 32 MFMAs take 12 ds_read_b64 instead of 24 4-byte reads.  The strides put the two lane halves of a b64 read
-// group (tiles kq, kq + 1: 2 positions or 1 window apart) on opposite halves of the 64 banks.
-constexpr int WG_CS = 48;                         // a1 position stride (32 channels + pad; 2 * 48 = 32 mod 64)
-constexpr int WG_A1 = 6 * A1 * WG_CS;             // one band's conv1 rows [6][26][48]
-constexpr int WG_VS = 80;                         // window stride of the staged (value, argmax) pairs (int2)
-constexpr int WG_PX = 3 * 16 * C2 + 16;           // one wave's P_i for one ci half: [3][16 ci][64 co] (+pad)
-
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) CONV_REGS void conv_wgrad_kernel(
-    const float* __restrict__ x, const int32_t* __restrict__ idx, const int32_t* __restrict__ cnt, int bmax,
-    int splits, const float* __restrict__ params, int64_t stride, const float* __restrict__ dPool,
-    const uint8_t* __restrict__ code, float* __restrict__ w2_part) {
-  __shared__ float smem[(WG_A1 + 24 * WG_VS * 2 > 4 * WG_PX) ? WG_A1 + 24 * WG_VS * 2 : 4 * WG_PX];
-  __shared__ float img_s[IMG * IMG];
-  __shared__ float gb_s[4][C2];
-  __shared__ float w1_s[10 * C1];      // conv1's taps and bias for the 16x16x4 recompute pieces (read every band)
-  float* const a1_s = smem;            // [6][26][WG_CS]
-  int2* const vq_s = reinterpret_cast<int2*>(smem + WG_A1);  // [24 windows][WG_VS]: (value bits, argmax)
-  const int sp = blockIdx.x;
-  const int r = blockIdx.y;
-  const int count = cnt[r];
-  // samples [sp*WG_SAMPLES, (sp+1)*WG_SAMPLES): the split of a replica depends only on its own batch,
-  // so its summation order (and v(S)) does not depend on which other replicas share the launch
-  const int j_begin = sp * WG_SAMPLES;
-  const int j_end = min(count, j_begin + WG_SAMPLES);
-  if (j_begin >= j_end) return;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int m = lane & 31;
-  const int kh = lane >> 5;
-  const float* P = params + (int64_t)r * stride;
-  float w1r[5];
-  load_w1r(P, kh, m, w1r);
-  if (MPLC_W1_LDS)
-    for (int e = tid; e < 10 * C1; e += WG_THREADS) w1_s[e] = e < 9 * C1 ? P[OFF_W1 + e] : P[OFF_B1 + e - 9 * C1];
-  float gb = 0.0f;  // db2 partial of channel tid & 63 (every pair this thread stages has that channel)
-  float pdv[WG_PRE];
-  uint32_t pcd[WG_PRE];
-  // window rows 2*band, 2*band+1 of sample jj: pair e = tid + 256*s is element 24*64*band + e (contiguous)
-  auto fetch = [&](int jj, int band) {
-    const int64_t base = ((int64_t)r * bmax + jj) * FEAT + band * 2 * PL * C2;
-#pragma unroll
-    for (int s = 0; s < WG_PRE; ++s) {
-      const int e = tid + WG_THREADS * s;
-      pdv[s] = dPool[base + e];
-      pcd[s] = code[base + e];
-    }
-  };
-  constexpr int IMG_PRE = (IMG * IMG + WG_THREADS - 1) / WG_THREADS;
-  float imgv[IMG_PRE];
-  auto fetch_img = [&](int jj) {
-    const float* xr = x + (int64_t)idx[(int64_t)r * bmax + jj] * (IMG * IMG);
-#pragma unroll
-    for (int k = 0; k < IMG_PRE; ++k) {
-      const int e = tid + WG_THREADS * k;
-      imgv[k] = xr[e < IMG * IMG ? e : 0];
-    }
-  };
-  // GEMM roles: wave = transform row i; lane (tl = lane & 15: ci / co in a group of 16, kq = lane >> 4: tile)
-  const int wi = wave;
-  const int tl = lane & 15, kq = lane >> 4;
-  // B^T row i (input transform) combines patch rows (ra, rb) with signs (sa, sb); A row i (gradient
-  // transform) picks delta's row dy with factor A[i][dy]
-  fvec4 acc[4][2][4];  // [j][ci half][co group]
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-      for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-  fetch(j_begin, 0);
-  fetch_img(j_begin);
-  // the sample loop compiled once per wave (MPLC_WSPEC): signs of B^T and A's row are compile-time constants
-  auto samples = [&](auto wtag) __attribute__((always_inline)) {
-  constexpr int WIC = decltype(wtag)::value;
-  const int wv = WIC >= 0 ? WIC : wi;
-  const int ra = (wv == 0) ? 0 : 1;
-  const int rb = (wv == 3) ? 3 : 2;
-  const float sa = (wv == 2) ? -1.0f : 1.0f;
-  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
-  const float ai0 = (wv == 3) ? 0.0f : 1.0f;                       // A[i][0]
-  const float ai1 = (wv == 0) ? 0.0f : ((wv == 1) ? 1.0f : -1.0f);  // A[i][1]
-  for (int j = j_begin; j < j_end; ++j) {
-    for (int band = 0; band < 6; ++band) {
-      __syncthreads();  // previous band's readers (a1_s, vq_s; and img_s by its staging) done
-      if (band == 0) {
-#pragma unroll
-        for (int k = 0; k < IMG_PRE; ++k)
-          if (tid + WG_THREADS * k < IMG * IMG) img_s[tid + WG_THREADS * k] = imgv[k];
-        if (j + 1 < j_end) fetch_img(j + 1);
-        __syncthreads();
-      }
-      // windows of the band: (value masked by the positive bit, argmax)
-#pragma unroll
-      for (int s = 0; s < WG_PRE; ++s) {
-        const int e = tid + WG_THREADS * s;  // window e >> 6 of the band (row-major), channel e & 63
-        const uint32_t c = pcd[s];
-        const float v = (c & 0x80) ? pdv[s] : 0.0f;
-        gb += v;
-        vq_s[(e >> 6) * WG_VS + (e & 63)] = int2{__float_as_int(v), (int)(c & 3)};
-      }
-      // conv1 + ReLU of rows 4*band .. 4*band+5: 156 positions = 4 tiles of 32 (one per wave, 32x32x2) and the
-      // last 28 positions as 2 x 16 positions x 2 channel halves on 16x16x4 (one piece per wave; a fifth 32x32
-      // tile on wave 0 was 1/8 padding and doubled that wave's share).  Taps and bias in conv1_mfma's k order on
-      // both forms (an exact fmaf chain): bit-identical activations.
-#ifndef WG_EXP_NOCONV1  // timing experiment switch (garbage results): conv1 recompute compiled out
-      {
-        const int p = wave * 32 + m;
-        const floatx16 a = conv1_mfma(img_s, (4 * band + p / A1) * IMG + p % A1, kh, w1r);
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          a1_s[(wave * 32 + acc_row(reg, kh)) * WG_CS + 2 * (m & 15) + (m >> 4)] = fmaxf(a[reg], 0.0f);
-      }
-      {
-        const int mt = wave >> 1, h = wave & 1, tl = lane & 15, kq = lane >> 4;
-        const int p = min(128 + 16 * mt + tl, 6 * A1 - 1);
-        fvec4 c1 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) {
-          const int k = 4 * s3 + kq;
-          const float av = (k < 9) ? img_s[(4 * band + p / A1 + k / 3) * IMG + p % A1 + k % 3] : ((k == 9) ? 1.0f : 0.0f);
-          const float wv = MPLC_W1_LDS ? ((k < 10) ? w1_s[k * C1 + 16 * h + tl] : 0.0f)
-                                       : ((k < 9) ? P[OFF_W1 + k * C1 + 16 * h + tl]
-                                                  : ((k == 9) ? P[OFF_B1 + 16 * h + tl] : 0.0f));
-          c1 = mfma16(av, wv, c1);
-        }
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {  // rows past 155 are position 155 again: the same value rewritten
-          const int pw = min(128 + 16 * mt + 4 * kq + reg, 6 * A1 - 1);
-          a1_s[pw * WG_CS + 2 * tl + h] = fmaxf(c1[reg], 0.0f);
-        }
-      }
-#endif
-      if (band < 5) fetch(j, band + 1);
-      else if (j + 1 < j_end) fetch(j + 1, 0);
-      __syncthreads();
-      // 6 k-steps of 4 tiles (window (wr, wc) = tile 12*wr + wc of the band; lane kq takes tile 4*st + kq)
-#pragma unroll 1
-#ifdef WG_EXP_NOGEMM  // timing experiment switch (garbage results; the dead staging is compiled out with it)
-      for (int st = 0; st < 0; ++st) {
-#else
-      for (int st = 0; st < 6; ++st) {
-#endif
-        const int tb = 4 * st + kq;
-        const int wr = tb / PL, wc = tb % PL;
-        // V: B^T d B of the tile's 4x4 conv1 patch (rows 2*wr .., columns 2*wc ..), channels tl, 16 + tl
-        const fvec2* d0 = reinterpret_cast<const fvec2*>(a1_s + ((2 * wr + ra) * A1 + 2 * wc) * WG_CS) + tl;
-        const int drow = (rb - ra) * A1 * (WG_CS / 2);
-        fvec2 pa[4], pb[4];  // rows ra, rb of the patch, columns c: (ci tl, ci 16 + tl)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          pa[c] = d0[c * (WG_CS / 2)];
-          pb[c] = d0[drow + c * (WG_CS / 2)];
-        }
-        float va[2][4];
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch) {
-          float t[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if constexpr (WIC >= 0)
-              t[c] = (WIC == 2 ? -pa[c][ch] : pa[c][ch]) + (WIC == 0 || WIC == 3 ? -pb[c][ch] : pb[c][ch]);
-            else
-              t[c] = sa * pa[c][ch] + sb * pb[c][ch];
-          }
-          va[ch][0] = t[0] - t[2];
-          va[ch][1] = t[1] + t[2];
-          va[ch][2] = t[2] - t[1];
-          va[ch][3] = t[1] - t[3];
-        }
-        // D: delta's single nonzero v at (dy, dx): D[i][j] = v * A[i][dy] * A[j][dx], channels 16*cg + tl
-        float db[4][4];
-#pragma unroll
-        for (int cg = 0; cg < 4; ++cg) {
-          const int2 vs = vq_s[tb * WG_VS + 16 * cg + tl];
-          const float v = __int_as_float(vs.x);
-          const int sl = vs.y;
-          float vi;
-          if constexpr (WIC == 0) vi = (sl & 2) ? 0.0f : v;
-          else if constexpr (WIC == 1) vi = v;
-          else if constexpr (WIC == 2) vi = (sl & 2) ? -v : v;
-          else if constexpr (WIC == 3) vi = (sl & 2) ? -v : 0.0f;
-          else vi = ((sl & 2) ? ai1 : ai0) * v;
-          const bool dx = (sl & 1) != 0;
-          db[cg][0] = dx ? 0.0f : vi;
-          db[cg][1] = vi;
-          db[cg][2] = dx ? -vi : vi;
-          db[cg][3] = dx ? -vi : 0.0f;
-        }
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-          for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-            for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = mfma16(va[ch][jj], db[cg][jj], acc[jj][ch][cg]);
-      }
-    }
-  }
-  };
-  if constexpr (MPLC_WSPEC) {
-    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
-      case 0: samples(IntC<0>{}); break;
-      case 1: samples(IntC<1>{}); break;
-      case 2: samples(IntC<2>{}); break;
-      default: samples(IntC<3>{}); break;
-    }
-  } else {
-    samples(IntC<-1>{});
-  }
-  // inverse transform dW2[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]: wave i folds
-  // its row (P_i0 = M_i0 + .5 M_i1 + .5 M_i2, P_i1 = .5 M_i1 - .5 M_i2, P_i2 = .5 M_i1 + .5 M_i2 + M_i3), the
-  // waves exchange P through LDS, one ci half at a time.  Lane holds ci 16*ch + 4*kq + rr, co 16*cg + tl.
-  gb_s[wave][lane] = gb;
-  float* out = w2_part + ((int64_t)r * splits + sp) * MPLC_CNN_W2P;
-#pragma unroll
-  for (int ch = 0; ch < 2; ++ch) {
-    __syncthreads();  // previous readers of smem (the last band, or the previous half) done
-    float* px = smem + wi * WG_PX;
-#pragma unroll
-    for (int cg = 0; cg < 4; ++cg)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float m0 = acc[0][ch][cg][rr], m1 = acc[1][ch][cg][rr], m2 = acc[2][ch][cg][rr],
-                    m3 = acc[3][ch][cg][rr];
-        const int o = (4 * kq + rr) * C2 + 16 * cg + tl;
-        px[o] = (m0 + 0.5f * m1) + 0.5f * m2;
-        px[16 * C2 + o] = 0.5f * m1 - 0.5f * m2;
-        px[32 * C2 + o] = (0.5f * m1 + 0.5f * m2) + m3;
-      }
-    __syncthreads();
-    for (int e = tid; e < 16 * C2; e += WG_THREADS) {  // (ci in half, co)
-      const int ci = 16 * ch + (e >> 6), co = e & 63;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const float p0 = smem[0 * WG_PX + kx * 16 * C2 + e], p1 = smem[1 * WG_PX + kx * 16 * C2 + e];
-        const float p2 = smem[2 * WG_PX + kx * 16 * C2 + e], p3 = smem[3 * WG_PX + kx * 16 * C2 + e];
-        const float w0 = (p0 + 0.5f * p1) + 0.5f * p2;
-        const float w1 = 0.5f * p1 - 0.5f * p2;
-        const float w2 = (0.5f * p1 + 0.5f * p2) + p3;
-        out[((0 * 3 + kx) * C1 + ci) * C2 + co] = w0;
-        out[((1 * 3 + kx) * C1 + ci) * C2 + co] = w1;
-        out[((2 * 3 + kx) * C1 + ci) * C2 + co] = w2;
-      }
-    }
-  }
-  if (tid < C2) out[9 * C1 * C2 + tid] = (gb_s[0][tid] + gb_s[1][tid]) + (gb_s[2][tid] + gb_s[3][tid]);
-}
-
 // Adam on W1 | b1 | W2 | b2 (params [0, 18816)) from the per-sample / per-split partial gradients.
 __global__ void adam_small_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ adam_t, int bmax,
                                   int splits, const float* __restrict__ w1_part, const float* __restrict__ w2_part,
@@ -1685,40 +1294,54 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
   const float* P = params + (int64_t)mdl * stride;
   for (int e = tid; e < HID * NCLS + NCLS; e += 256) w4_s[e] = P[OFF_W4 + e];
   __syncthreads();
-  double lsum = 0.0;
+  // The loss is summed in fixed blocks of 256 samples (the tree below), added to the model's running total in
+  // block order: with every chunk but the last a multiple of 256 samples (the host's rule), the total is the same
+  // bits whatever the chunk size - and the chunk size depends on how many models share the evaluation.
+  double run = (tid == 0) ? loss_sum[mdl] : 0.0;
   int csum = 0;
-  for (int jj = tid; jj < count; jj += 256) {
-    const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
-    float z[NCLS];
+  for (int b0 = 0; b0 < count; b0 += 256) {
+    const int jj = b0 + tid;
+    double lv = 0.0;
+    if (jj < count) {
+      const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
+      float z[NCLS];
 #pragma unroll
-    for (int o = 0; o < NCLS; ++o) z[o] = w4_s[HID * NCLS + o];
-    for (int c = 0; c < HID; ++c) {
-      const float hv = h[c];
+      for (int o = 0; o < NCLS; ++o) z[o] = w4_s[HID * NCLS + o];
+      for (int c = 0; c < HID; ++c) {
+        const float hv = h[c];
 #pragma unroll
-      for (int o = 0; o < NCLS; ++o) z[o] += hv * w4_s[c * NCLS + o];
+        for (int o = 0; o < NCLS; ++o) z[o] += hv * w4_s[c * NCLS + o];
+      }
+      int am = 0;
+      float mx = z[0];
+#pragma unroll
+      for (int o = 1; o < NCLS; ++o)
+        if (z[o] > mx) { mx = z[o]; am = o; }
+      float s = 0.0f;
+#pragma unroll
+      for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
+      const int y = labels[row_base + jj];
+      lv = (double)(logf(s) + mx - z[y]);
+      csum += (am == y) ? 1 : 0;
     }
-    int am = 0;
-    float mx = z[0];
-#pragma unroll
-    for (int o = 1; o < NCLS; ++o)
-      if (z[o] > mx) { mx = z[o]; am = o; }
-    float s = 0.0f;
-#pragma unroll
-    for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
-    const int y = labels[row_base + jj];
-    lsum += (double)(logf(s) + mx - z[y]);
-    csum += (am == y) ? 1 : 0;
+    ls[tid] = lv;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+      if (tid < off) ls[tid] += ls[tid + off];
+      __syncthreads();
+    }
+    if (tid == 0) run += ls[0];
+    __syncthreads();  // ls is rewritten by the next block
   }
-  ls[tid] = lsum;
   cs[tid] = csum;
   __syncthreads();
   for (int off = 128; off >= 1; off >>= 1) {
-    if (tid < off) { ls[tid] += ls[tid + off]; cs[tid] += cs[tid + off]; }
+    if (tid < off) cs[tid] += cs[tid + off];
     __syncthreads();
   }
   if (tid == 0) {
     correct[mdl] += cs[0];
-    loss_sum[mdl] += ls[0];
+    loss_sum[mdl] = run;
   }
 }
 
@@ -1835,8 +1458,8 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                                           t->code, t->w1_part);
   PROF_END(5);
   PROF_BEGIN(6);
-  conv_wgrad_kernel<<<dim3(t->w2_splits, R), WG_THREADS, 0, s>>>(t->x, t->idx, t->cnt, B, t->w2_splits, t->params,
-                                                                 S, t->dpooled, t->code, t->w2_part);
+  mplc_mnist::launch_conv_wgrad(t->w2_splits, R, s, t->x, t->idx, t->cnt, B, t->params, S, t->dpooled, t->code,
+                                t->w2_part);
   PROF_END(6);
   PROF_BEGIN(7);
   adam_small_kernel<<<dim3((OFF_W3 + 255) / 256, R), 256, 0, s>>>(t->cnt, t->adam_t, B, t->w2_splits, t->w1_part,

@@ -12,6 +12,7 @@ import ctypes
 import numpy as np
 
 from . import _native
+from .cnn import eval_plan
 
 STRIDE = 1251008
 NPARAM = 1250954
@@ -81,6 +82,7 @@ def layout_items():
 class CifarModel:
     """Model hooks (see mplc.cnn.MnistModel) for the CIFAR10 CNN."""
     name = "cifar10_cnn"
+    EVAL_SAMPLE_BYTES, EVAL_MODEL_BYTES = EVAL_FLOATS * 4, WT * 4  # evaluation workspace (mplc_cifar_evaluate)
     STRIDE, NPARAM = STRIDE, NPARAM
     # Keras get_weights() order (mplc/dataset.py:170-190): (offset in a model row, shape)
     KERAS_LAYERS = ((0, (3, 3, 3, 32)), (896, (32,)), (960, (3, 3, 32, 32)), (10176, (32,)), (10240, (3, 3, 32, 64)),
@@ -195,15 +197,16 @@ class CifarModel:
         stream = _native.stream_handle(dev)
         n = int(y.numel())
         C = sel.shape[0]
-        # the workspace also holds every model's Winograd weights (C * WT floats, mplc_cifar_eval_workspace_floats):
-        # the activation chunk gets the rest of the budget
-        budget = max(0, eng.eval_budget_bytes - C * WT * 4)
-        chunk = int(max(16, min(n, budget // max(1, C * EVAL_FLOATS * 4))))
-        chunk = min(chunk, 65535)
-        ws = torch.empty(int(self.lib.mplc_cifar_eval_workspace_floats(C, chunk)), dtype=torch.float32, device=dev)
+        # the workspace also holds every model's Winograd weights (WT floats per model,
+        # mplc_cifar_eval_workspace_floats); cnn.eval_plan keeps the loss sums independent of C
+        chunk, group = eval_plan(n, C, self.EVAL_SAMPLE_BYTES, self.EVAL_MODEL_BYTES, eng.eval_budget_bytes)
+        ws = torch.empty(int(self.lib.mplc_cifar_eval_workspace_floats(group, chunk)), dtype=torch.float32, device=dev)
         correct = torch.zeros(C, dtype=torch.int32, device=dev)
         loss = torch.zeros(C, dtype=torch.float64, device=dev)
-        _native.check(self.lib.mplc_cifar_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n,
-                                                   chunk, _native.ptr(ws), _native.ptr(correct), _native.ptr(loss),
-                                                   stream), "mplc_cifar_evaluate")
+        for g0 in range(0, C, group):
+            g = min(group, C - g0)
+            _native.check(self.lib.mplc_cifar_evaluate(_native.ptr(sel[g0:g0 + g]), STRIDE, g, _native.ptr(x),
+                                                       _native.ptr(y), n, chunk, _native.ptr(ws),
+                                                       _native.ptr(correct[g0:g0 + g]), _native.ptr(loss[g0:g0 + g]),
+                                                       stream), "mplc_cifar_evaluate")
         return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n

@@ -179,11 +179,32 @@ def minibatch_bounds(n, M):
     return [0] + [int(v) for v in inner] + [int(n)]
 
 
+EVAL_BLOCK = 256  # the evaluation kernels sum the loss in fixed blocks of this many samples
+
+
+def eval_plan(n, C, sample_bytes, model_bytes, budget):
+    """(chunk, group) of an evaluation of C models on n samples within `budget` bytes of workspace: models are
+    evaluated `group` at a time, each chunk of samples holding sample_bytes per (model, sample) plus model_bytes
+    per model.  Every chunk but the last is a multiple of EVAL_BLOCK samples, so the kernels' loss sums (fixed
+    256-sample blocks in sample order, mplc_cnn_evaluate / mplc_cifar_evaluate) do not depend on C, the budget or
+    which models share the evaluation: a model's val loss - what the early-stopping rule compares - is a function
+    of the model alone."""
+    cap = max(0, budget - C * model_bytes) // max(1, C * sample_bytes)
+    if cap >= n and n <= 65535:
+        return n, C
+    if cap >= EVAL_BLOCK:
+        return min(cap, 65535) // EVAL_BLOCK * EVAL_BLOCK, C
+    chunk = min(n, EVAL_BLOCK)
+    group = max(1, budget // (chunk * sample_bytes + model_bytes))
+    return chunk, min(C, group)
+
+
 class MnistModel:
     """Model hooks of the batched MNIST CNN (csrc/mnist_cnn.hip): parameter layout, optimizer state,
     workspaces, one lockstep step, evaluation.  TrainBatch / CnnBatchTrainer drive any model with these."""
     name = "mnist_cnn"
     STRIDE, NPARAM = STRIDE, NPARAM
+    EVAL_SAMPLE_BYTES, EVAL_MODEL_BYTES = (FEAT + HID) * 4, W2T * 4  # evaluation workspace (mplc_cnn_evaluate)
     KERAS_LAYERS = KERAS_LAYERS
     KERNEL_IDS = KERNEL_IDS
     input_shape = (28, 28)
@@ -300,17 +321,18 @@ class MnistModel:
         stream = _native.stream_handle(dev)
         n = int(y.numel())
         C = sel.shape[0]
-        chunk = int(max(32, min(n, eng.eval_budget_bytes // max(1, C * (FEAT + HID) * 4))))
-        chunk = min(chunk, 65535)
-        pooled = torch.empty((C, chunk, FEAT), dtype=torch.float32, device=dev)
-        hidden = torch.empty((C, chunk, HID), dtype=torch.float32, device=dev)
+        chunk, group = eval_plan(n, C, self.EVAL_SAMPLE_BYTES, self.EVAL_MODEL_BYTES, eng.eval_budget_bytes)
+        pooled = torch.empty((group, chunk, FEAT), dtype=torch.float32, device=dev)
+        hidden = torch.empty((group, chunk, HID), dtype=torch.float32, device=dev)
         correct = torch.zeros(C, dtype=torch.int32, device=dev)
         loss = torch.zeros(C, dtype=torch.float64, device=dev)
-        wino = torch.empty((C, W2T), dtype=torch.float32, device=dev)
-        _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel), STRIDE, C, _native.ptr(x), _native.ptr(y), n, chunk,
-                                                 _native.ptr(pooled), _native.ptr(hidden), _native.ptr(wino),
-                                                 _native.ptr(correct),
-                                                 _native.ptr(loss), stream), "mplc_cnn_evaluate")
+        wino = torch.empty((group, W2T), dtype=torch.float32, device=dev)
+        for g0 in range(0, C, group):
+            g = min(group, C - g0)
+            _native.check(self.lib.mplc_cnn_evaluate(_native.ptr(sel[g0:g0 + g]), STRIDE, g, _native.ptr(x),
+                                                     _native.ptr(y), n, chunk, _native.ptr(pooled), _native.ptr(hidden),
+                                                     _native.ptr(wino), _native.ptr(correct[g0:g0 + g]),
+                                                     _native.ptr(loss[g0:g0 + g]), stream), "mplc_cnn_evaluate")
         return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
 
 

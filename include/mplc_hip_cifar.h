@@ -162,7 +162,9 @@ int mplc_cifar_init_params(float* params, int64_t stride, const uint64_t* keys, 
 int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream);
 
 /* Forward-only (inference: no dropout) evaluation of n_models models on samples [0, n_samples):
- * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  ws is a workspace of
+ * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64: per
+ * block of 256 samples a fixed tree, the blocks added in sample order; with every chunk but the last a multiple
+ * of 256 the sum does not depend on chunk or n_models).  ws is a workspace of
  * mplc_cifar_eval_workspace_floats(n_models, chunk) floats. */
 int64_t mplc_cifar_eval_workspace_floats(int n_models, int chunk);
 int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,

@@ -186,7 +186,9 @@ int mplc_seq_snapshot(const float* params, int64_t stride, int64_t n_param, cons
                       int epochs, const int32_t* snap_first, float* snap, void* stream);
 
 /* Forward-only evaluation of n_models models on samples [0, n_samples) of x/labels:
- * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64).  pooled/hidden/w2_wino are
+ * correct[m] += #argmax hits, loss_sum[m] += sum of per-sample CE (float64: per
+ * block of 256 samples a fixed tree, the blocks added in sample order; with every chunk but the last a multiple
+ * of 256 the sum does not depend on chunk or n_models).  pooled/hidden/w2_wino are
  * workspaces of n_models * chunk * 9216, n_models * chunk * 128 and n_models * MPLC_CNN_W2T floats. */
 int mplc_cnn_evaluate(const float* params, int64_t stride, int n_models, const float* x, const int32_t* labels,
                       int n_samples, int chunk, float* pooled, float* hidden, float* w2_wino, int32_t* correct,

@@ -237,9 +237,10 @@ def evaluate(p, x, y, batch=1000):
     """[mean CE, accuracy] like Keras evaluate (mplc/multi_partner_learning.py:142-169)."""
     torch = _torch()
     correct, loss = 0, 0.0
+    dt = p["W1"].dtype  # fp64 parameters (precise runs) evaluate in fp64
     with torch.no_grad():
         for s in range(0, len(y), batch):
-            z = forward(p, x[s:s + batch])
+            z = forward(p, x[s:s + batch].to(dt))
             loss += float(torch.nn.functional.cross_entropy(z, y[s:s + batch], reduction="sum"))
             correct += int((z.argmax(1) == y[s:s + batch]).sum())
     return loss / len(y), correct / len(y)
@@ -324,14 +325,21 @@ HISTORY_METRICS = ("val_accuracy", "val_loss", "loss", "accuracy")
 
 def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1, M=10,
                     aggregation="data-volume", early_stopping=False, return_model=False, approach="fedavg",
-                    history=None, es_trace=None):
+                    history=None, es_trace=None, precise=False):
     """v(S) of one coalition, the reference's way (sequential), on the engine's keyed init and order.
     With a `history` dict, the learning history (mplc/mpl_utils.py:11-27) is recorded into it; with an
-    `es_trace` list, the val losses the early-stopping rule compares are appended to it."""
+    `es_trace` list, the val losses the early-stopping rule compares are appended to it.  precise=True (FedAvg
+    and singletons): the same schedule and fp32 constants with every tensor operation in float64 - gradients,
+    Adam, the average (kept in fp64) and the test evaluation: the high-precision value of the same algorithm."""
     torch = _torch()
     coalition = tuple(sorted(coalition))
     mask = sum(1 << p for p in coalition)
     glob = unpack(init_params(init_key(seed, mask)))
+    dt = torch.float64 if precise else None
+    if precise:
+        if approach != "fedavg" or history is not None:
+            raise ValueError("precise=True restates FedAvg / singleton training without history")
+        glob = {k: v.to(dt) for k, v in glob.items()}
     epochs_done = epochs
     if history is not None:
         for p_id in coalition:
@@ -342,13 +350,13 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
         p_id = coalition[0]
         key = shuffle_key(seed, mask, p_id)
         params = {k: v.clone() for k, v in glob.items()}
-        opt = KerasAdam(params)
+        opt = KerasAdam(params, precise=precise)
         best, wait = np.inf, 0
         log = None
         for e in range(epochs):
             log = _FitLog() if history is not None else None
             for rows in single_epoch_rows(key, partner_rows[p_id], batch_sizes[p_id], e):
-                g, lm = gradients(params, data.x_train[rows], data.y_train[rows])
+                g, lm = gradients(params, data.x_train[rows], data.y_train[rows], dtype=dt)
                 if log is not None:
                     log.batch(params, data.x_train[rows], data.y_train[rows], lm)
                 opt.step(params, g)
@@ -409,21 +417,21 @@ def coalition_value(data, partner_rows, batch_sizes, coalition, seed=0, epochs=1
                 for p_id in coalition:
                     key = shuffle_key(seed, mask, p_id)
                     params = {k: v.clone() for k, v in glob.items()}
-                    opt = KerasAdam(params)  # fresh optimizer per partner fit
+                    opt = KerasAdam(params, precise=precise)  # fresh optimizer per partner fit
                     log = _FitLog() if history is not None else None
                     for rows in fedavg_round_rows(key, partner_rows[p_id], batch_sizes[p_id], M, e, m):
-                        g, lm = gradients(params, data.x_train[rows], data.y_train[rows])
+                        g, lm = gradients(params, data.x_train[rows], data.y_train[rows], dtype=dt)
                         if log is not None:
                             log.batch(params, data.x_train[rows], data.y_train[rows], lm)
                         opt.step(params, g)
                     if log is not None:
                         log.store(history[p_id], e, m, params, data)
                     partner_models.append(params)
-                glob = average_models(glob, partner_models, w)
+                glob = average_models(glob, partner_models, w, keep_f64=precise)
             if early_stopping and epochs > PATIENCE and e >= PATIENCE and val_hist[e] > val_hist[e - PATIENCE]:
                 epochs_done = e + 1
                 break
     _, acc = evaluate(glob, data.x_test, data.y_test)
-    if return_model:
-        return acc, epochs_done, pack(glob)
+    if return_model:  # a model row; precise runs return the fp64 tensors themselves
+        return acc, epochs_done, ({k: v.detach().clone() for k, v in glob.items()} if precise else pack(glob))
     return acc, epochs_done

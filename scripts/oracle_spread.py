@@ -1,0 +1,50 @@
+"""ORACLE fixtures (test infrastructure): the oracle's own spread of v(S) over fp32 summation orders.
+
+    python scripts/oracle_spread.py config1_3p|config1_2p|config3 [threads ...]
+
+The CNN oracle (oracle/cnn.py, torch-CPU fp32) is not reproducible below about a point for a single coalition:
+its summation order changes with the CPU thread count, and a model still in the steep part of learning ends on
+either side of a near-tie (a max-pool window or a ReLU input at ~0).  scripts/diag_config1.py measured it on the
+GPU box for config #1's 3-partner variant: coalition (0, 1) gives 0.9585 ... 0.9734 over 1 .. 16 threads (fp64:
+0.9718), the device 0.9585.  A per-coalition gate therefore needs that spread, sampled over many thread counts,
+which is too slow to recompute inside a GPU test: this script computes it once (CPU only) and writes
+tests/golden/oracle_spread_<name>.json; the GPU tests add one live oracle run at the box's thread count.
+
+Scenarios (the GPU tests' own, deterministic data: numpy-seeded synthetic images):
+  config1_3p / config1_2p  tests/test_config1_gpu.py: the reference's contrib yml (MNIST, dataset_proportion 0.1,
+                           E=1, M=10, G=8) with [0.2, 0.5, 0.3] / [0.1, 0.9], synthetic MNIST signal 0.3 as uint8
+  config3                  tests/test_workload_gpu.py: 10 partners x 0.1, signal 0.2, E=1, M=20, G=8; the 18
+                           coalitions of test_config3_small_coalitions_vs_oracle
+Also written: the fp64 value (oracle coalition_value(precise=True)) and a CRC of the data the values belong to."""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "distributed-learning-contributivity_amd")):
+    sys.path.insert(0, p)
+from spread_fixtures import GOLDEN, data_crc, oracle_values, scenario  # noqa: E402
+
+
+def main():
+    name = sys.argv[1]
+    threads = [int(v) for v in sys.argv[2:]] or [1, 2, 3, 4, 6, 8, 12, 16]
+    sc, coals = scenario(name)
+    out = {"scenario": name, "generator": "scripts/oracle_spread.py", "data_crc32": data_crc(sc),
+           "coalitions": [list(k) for k in coals], "threads": threads, "fp32": {}}
+    t0 = time.time()
+    for th in threads:
+        out["fp32"][str(th)] = oracle_values(sc, coals, th)
+        print(name, "threads", th, ["%.4f" % v for v in out["fp32"][str(th)]], "%.0fs" % (time.time() - t0), flush=True)
+    out["fp64"] = oracle_values(sc, coals, 8, precise=True)
+    print(name, "fp64", ["%.4f" % v for v in out["fp64"]], flush=True)
+    path = os.path.join(GOLDEN, f"oracle_spread_{name}.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", path, "%.0fs" % (time.time() - t0))
+
+
+if __name__ == "__main__":
+    main()

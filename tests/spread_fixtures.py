@@ -1,0 +1,98 @@
+"""Scenarios and oracle spreads shared by the accuracy gates of tests/test_config1_gpu.py and
+tests/test_workload_gpu.py and by scripts/oracle_spread.py, which writes the fixtures
+tests/golden/oracle_spread_<name>.json (the oracle's v(S) over many CPU thread counts, i.e. fp32 summation
+orders, and in fp64).  Test infrastructure: it runs the oracle (oracle/cnn.py) only as the checker."""
+import json
+import os
+import tempfile
+import zlib
+from itertools import combinations
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+CONFIG3_COALS = [(p,) for p in range(10)] + [(2, 7), (0, 9), (4, 5), (1, 3), (6, 8), (0, 5), (2, 9), (3, 7)]
+
+
+def config1_scenario(amounts, signal=0.3):
+    """The scenario main.py builds from the contrib yml with `amounts` (synthetic MNIST as mnist.npz)."""
+    from mplc.dataset import _synthetic_images
+    from mplc.scenario import Scenario
+    d = tempfile.mkdtemp(prefix="cfg1_")
+    x, y, xt, yt = _synthetic_images((28, 28, 1), 60000, 10000, 0, signal)
+    q = lambda a: np.round(a[..., 0] * 255).astype(np.uint8)  # noqa: E731  (the real file's uint8 pixels)
+    np.savez(os.path.join(d, "mnist.npz"), x_train=q(x), y_train=np.argmax(y, 1).astype(np.uint8), x_test=q(xt),
+             y_test=np.argmax(yt, 1).astype(np.uint8))
+    old = os.environ.get("MPLC_DATA_DIR")
+    os.environ["MPLC_DATA_DIR"] = d
+    try:
+        sc = Scenario(len(amounts), list(amounts), dataset_name="mnist", dataset_proportion=0.1,
+                      samples_split_option=["basic", "random"], epoch_count=1, minibatch_count=10,
+                      gradient_updates_per_pass_count=8).provision()
+    finally:
+        if old is None:
+            os.environ.pop("MPLC_DATA_DIR", None)
+        else:
+            os.environ["MPLC_DATA_DIR"] = old
+    return sc
+
+
+def config3_scenario():
+    from mplc.dataset import Mnist
+    from mplc.scenario import Scenario
+    return Scenario(10, [0.1] * 10, dataset=Mnist(synthetic=True, signal=0.2), minibatch_count=20,
+                    gradient_updates_per_pass_count=8, epoch_count=1, is_early_stopping=False).provision()
+
+
+def scenario(name):
+    if name == "config1_3p":
+        sc = config1_scenario([0.2, 0.5, 0.3])
+        return sc, [k for r in range(1, 4) for k in combinations(range(3), r)]
+    if name == "config1_2p":
+        return config1_scenario([0.1, 0.9]), [(0,), (1,), (0, 1)]
+    if name == "config3":
+        return config3_scenario(), CONFIG3_COALS
+    raise ValueError(name)
+
+
+def data_crc(sc):
+    ds = sc.dataset
+    c = zlib.crc32(np.ascontiguousarray(ds.x_train).tobytes())
+    c = zlib.crc32(np.ascontiguousarray(np.asarray(ds.y_train)).tobytes(), c)
+    c = zlib.crc32(np.ascontiguousarray(ds.x_test).tobytes(), c)
+    for p in sc.partners_list:
+        c = zlib.crc32(np.ascontiguousarray(p.train_idx, dtype=np.int64).tobytes(), c)
+    return int(c)
+
+
+def oracle_values(sc, coals, threads, precise=False, seed=0):
+    import torch
+    from oracle import cnn as ocnn
+    ds = sc.dataset
+    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    prow = [p.train_idx for p in sc.partners_list]
+    bs = [p.batch_size for p in sc.partners_list]
+    t0 = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        return [float(ocnn.coalition_value(data, prow, bs, k, seed=seed, epochs=sc.epoch_count, M=sc.minibatch_count,
+                                           precise=precise)[0]) for k in coals]
+    finally:
+        torch.set_num_threads(t0)
+
+
+def golden_split(tag):
+    """The reference's own split of a BASELINE config (tests/golden/splits.json, made by make_golden.py)."""
+    with open(os.path.join(GOLDEN, "splits.json")) as f:
+        return next(r for r in json.load(f)["data"] if r["tag"] == tag)
+
+
+def load_spread(name, sc=None):
+    """The committed spread fixture of scenario `name` ({"coalitions", "fp32": {threads: values}, "fp64"});
+    with `sc`, checked to belong to that scenario's data and partition."""
+    with open(os.path.join(GOLDEN, f"oracle_spread_{name}.json")) as f:
+        rec = json.load(f)
+    if sc is not None:
+        assert rec["data_crc32"] == data_crc(sc), f"oracle_spread_{name}.json was made for other data"
+    return rec

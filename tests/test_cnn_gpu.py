@@ -186,6 +186,32 @@ def test_fedavg_aggregation_inside_training_is_np_average(scenario, engine):
     assert st.ws["w3src"].cpu().tolist() == [0, 0, 0]
 
 
+def test_eval_loss_independent_of_models_sharing_the_evaluation(engine):
+    """the summed loss of a model (the val loss the early-stopping rule compares) must not depend on how
+    many models share the evaluation or on the workspace budget - the chunk size follows both.  One model alone
+    with a budget for a single chunk, against the same model among 7 others with a budget of a few 256-sample
+    chunks (eval_plan then also splits the models into groups): bit-identical loss and hits."""
+    from mplc.cnn import eval_plan
+    st = engine.trainer.prepare([(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)], 1)
+    rows = st.glob.contiguous()
+    model = engine.model_impl
+    x, y = engine.x_train_d, engine.y_train_d
+    n = int(y.numel())
+    assert n > 1024
+    keep = engine.eval_budget_bytes
+    try:
+        engine.eval_budget_bytes = 8 << 30
+        c1, l1 = model.evaluate(engine, rows[3:4].contiguous(), x, y)
+        small = 150 << 20 if model.name == "cifar10_cnn" else 40 << 20
+        engine.eval_budget_bytes = small
+        chunk, group = eval_plan(n, 7, model.EVAL_SAMPLE_BYTES, model.EVAL_MODEL_BYTES, small)
+        assert chunk % 256 == 0 and chunk < n and group < 7, (chunk, group)
+        c7, l7 = model.evaluate(engine, rows, x, y)
+    finally:
+        engine.eval_budget_bytes = keep
+    assert c7[3] == c1[0] and l7[3] == l1[0], (c7[3], c1[0], l7[3], l1[0])
+
+
 def test_values_independent_of_batch_composition(engine):
     all7 = [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2), (0, 1, 2)]
     together = engine.evaluate(all7)

@@ -100,11 +100,13 @@ def test_layout_queries_match_host_constants_and_headers(model):
 
 def test_experiment_switches_refuse_product_builds(tmp_path):
     """A *_EXP_* timing switch (wrong results by design) is an #error unless MPLC_EXPERIMENT is defined."""
-    src = os.path.join(REPO, "distributed-learning-contributivity_amd", "csrc", "mnist_cnn.hip")
-    text = open(src).read()
+    csrc = os.path.join(REPO, "distributed-learning-contributivity_amd", "csrc")
+    src = os.path.join(csrc, "mnist_cnn.hip")
+    text = "".join(open(os.path.join(csrc, f)).read() for f in ("mnist_cnn.hip", "mnist_wgrad.hip"))
     switches = set(re.findall(r"#if(?:n?def)?\s*!?\s*(?:defined\()?(\w+_EXP_\w+)", text))
     assert switches, "no experiment switches found"
-    guard = text[:text.index("namespace {")]
+    common = open(os.path.join(csrc, "mnist_common.h")).read()  # both sources include it first
+    guard = common[:common.index("namespace {")]
     for sw in switches:
         assert f"defined({sw})" in guard, f"{sw} is not covered by the #error guard"
     hipcc = "/opt/rocm/bin/hipcc"
