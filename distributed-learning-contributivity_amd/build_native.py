@@ -102,6 +102,60 @@ def build(verbose=False, force=False, jobs=8, sanitize=False):
     return lib
 
 
+# Alternate kernel forms kept in the source because they are bit-identical to the product kernels (the matrix core
+# accumulates as an fma chain) and win at other batch sizes: the MFMA form of MNIST's dense1_bwd_adam
+# (MPLC_D1_MFMA=1) and the VALU form of CIFAR's dense5_bwd (MPLC_D5_MFMA=0).  build() links them into one variant
+# library, mplc/lib/variants/libmplc_hip_alt.so, which tests/test_variants_gpu.py runs against the product library
+# (bit-identical models), so the non-default bodies cannot rot unseen.
+VARIANTS = {"alt": {"mnist_cnn.hip": ["-DMPLC_D1_MFMA=1"], "cifar_cnn.hip": ["-DMPLC_D5_MFMA=0"]}}
+VARIANT_DIR = os.path.join(LIB_DIR, "variants")
+
+
+def build_variants(verbose=False, force=False, jobs=8):
+    """Variant libraries (VARIANTS): the listed sources recompiled with their flags, linked with the product objects
+    of every other source.  Call after build()."""
+    os.makedirs(VARIANT_DIR, exist_ok=True)
+    out = []
+    for name, flags in VARIANTS.items():
+        vdir = os.path.join(BUILD, "variant_" + name)
+        os.makedirs(vdir, exist_ok=True)
+        objs, todo = [], []
+        for src in sorted(glob.glob(os.path.join(CSRC, "*.hip"))):
+            base = os.path.basename(src)
+            if base in flags:
+                o = os.path.join(vdir, base[:-4] + ".o")
+                flag_file = o + ".flags"
+                stale = force or _stale(o, _deps(src)) or not os.path.exists(flag_file) or \
+                    open(flag_file).read() != " ".join(flags[base])
+                if stale:
+                    todo.append((src, o, flags[base], flag_file))
+            else:
+                o = os.path.join(BUILD, base[:-4] + ".o")
+            objs.append(o)
+
+        def comp(item):
+            src, o, fl, ff = item
+            cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + fl + ["-c", src, "-o", o]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for variant {name} {os.path.basename(src)}:\n{r.stderr}")
+            with open(ff, "w") as f:
+                f.write(" ".join(fl))
+        if todo:
+            with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+                list(ex.map(comp, todo))
+        lib = os.path.join(VARIANT_DIR, f"libmplc_hip_{name}.so")
+        if force or todo or _stale(lib, objs):
+            cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"link failed for variant {name}:\n{r.stderr}")
+        out.append(lib)
+    return out
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-v", "--verbose", action="store_true")
@@ -109,4 +163,6 @@ if __name__ == "__main__":
     ap.add_argument("--sanitize", action="store_true", help="host ASan/UBSan build into build/asan/")
     a = ap.parse_args()
     print(build(verbose=a.verbose, force=a.force, sanitize=a.sanitize))
+    if not a.sanitize:
+        print("\n".join(build_variants(verbose=a.verbose, force=a.force)))
     sys.exit(0)

@@ -216,6 +216,7 @@ __host__ __device__ constexpr int ci3_off(int k, int rowp) { return (k / 9) * ro
 // odd pixel stride, the 32 pixels of a tile fall on 32 distinct banks.
 template <int HI, int WI, int CI, int CO, int PAD, int BR, int NW, int UM, int EPI, int CS = 1>
 __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
+  static_assert(EPI == EPI_FWD || EPI == EPI_BWD_MASK, "the pooled-gradient epilogue (EPI_BWD_UNPOOL) is wino_kernel's");
   // CS channel slices: the input band is staged CI / CS channels at a time (K split), so a band (or a whole
   // sample) with many tiles per wave fits a small LDS footprint
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
@@ -411,7 +412,7 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
     const float* bias = (EPI == EPI_FWD) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
     const float* act = (EPI == EPI_BWD_MASK) ? a.aux + slot * (HO * WO * CO) : nullptr;
     const uint8_t* cd = (EPI == EPI_BWD_UNPOOL) ? a.code_in + slot * (HO * WO * CO) : nullptr;
-    float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * HO * WO * CO);
+    float* o = a.out + slot * (HO * WO * CO);
 #pragma unroll
     for (int u = 0; u < UM; ++u) {
       const int t = wave + NW * u;
@@ -429,16 +430,8 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
           const float v = acc[u][nt][reg];
           if constexpr (EPI == EPI_FWD) {
             o[o_i] = fmaxf(v + bv, 0.0f);
-          } else if constexpr (EPI == EPI_BWD_MASK) {
+          } else {
             o[o_i] = act[o_i] > 0.0f ? v : 0.0f;
-          } else {  // dropout' + un-pool into the dense dZ (2HO x 2WO) of the layer below
-            const uint32_t c = cd[o_i];
-            const float dv = (c & CODE_KEEP) ? v * SCALE_25 : 0.0f;
-            const bool pos = (c & CODE_POS) != 0;
-            const int sel = c & 3;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              o[((2 * y + (q >> 1)) * (2 * WO) + 2 * x + (q & 1)) * CO + ch] = (pos && sel == q) ? dv : 0.0f;
           }
         }
       }
@@ -656,26 +649,11 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
-#ifndef MPLC_WG_PIPE
-#define MPLC_WG_PIPE 0  // conv2's weight gradient: the next band's staging loads in flight during this band's MFMAs
-                        // (measured 115 vs 113-114 ms for the split staging without it: off)
-#endif
-#ifndef MPLC_WG_PIPE4
-#define MPLC_WG_PIPE4 1  // conv4's weight gradient likewise: -2 % (conv3's would spill 24 registers: not pipelined)
-#endif
-#ifndef MPLC_ROW_WSPEC
-#define MPLC_ROW_WSPEC 1  // wino_kernel: the group loop compiled per wave (compile-time B^T signs)
-#endif
+// Wave-index tag: a loop instantiated once per wave index (compile-time Winograd transform signs)
 template <int V>
 struct IntC {
   static constexpr int value = V;
 };
-#ifndef MPLC_FWD_BIAS_PRE
-#define MPLC_FWD_BIAS_PRE 1  // forward epilogues: bias loaded ahead (wave-local: last k-step; row form: LDS)
-#endif
-#ifndef MPLC_ROW_EPI_STAGE
-#define MPLC_ROW_EPI_STAGE 1  // wino_kernel: the data gradients' epilogue operand staged as bytes in LDS up front
-#endif
 template <int HI, int WI, int CI, int CO, int PAD, int BTY, int EPI, int UPI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_kernel(const ConvArgs a) {
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
@@ -698,20 +676,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // the data gradients' epilogue operand (EPI_BWD_MASK: the ReLU' mask a > 0; EPI_BWD_UNPOOL: the pool codes) for
   // the band's 2 BTY output rows, staged as bytes with the input band: its global loads share the staging's latency
   // instead of stalling the output phase of every group
-  constexpr bool STAGE_EPI = MPLC_ROW_EPI_STAGE && (EPI == EPI_BWD_MASK || EPI == EPI_BWD_UNPOOL);
+  constexpr bool STAGE_EPI = (EPI == EPI_BWD_MASK || EPI == EPI_BWD_UNPOOL);
   constexpr int ER = 2 * BTY;
   __shared__ float in_s[LR * ROWP];
   __shared__ float t_s[8 * TQ];
   __shared__ uint32_t e_s[STAGE_EPI ? ER * WO * CO / 4 : 1];
-  constexpr bool STAGE_BIAS = MPLC_FWD_BIAS_PRE && (EPI == EPI_FWD || POOL);
-  __shared__ float b_s[STAGE_BIAS ? CO : 1];  // the forward's bias, staged with the input band
+  constexpr bool STAGE_BIAS = (EPI == EPI_FWD || POOL);  // the forward's bias, staged with the input band
+  __shared__ float b_s[STAGE_BIAS ? CO : 1];
   const LogicalBlock lbk = xcd_block3();  // (band, sample, replica): a replica's blocks share one XCD's L2 (its U)
   const int band = lbk.x, j = lbk.y, r = lbk.z;
   const int count = a.cnt ? a.cnt[r] : a.cnt_all;
   if (j >= count) return;
   const int tid = threadIdx.x;
   const int64_t slot = (int64_t)r * a.bmax + j;
-  constexpr int IN_SZ = HI * WI * CI;
+  constexpr int IN_SZ = UPI ? (HI / 2) * (WI / 2) * CI : HI * WI * CI;  // UPI: a pooled gradient's slots
   const float* src = a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ : a.in + slot * IN_SZ;
   const int ty0 = band * BTY;
   const int bty = min(BTY, TYT - ty0);  // tile rows of this band
@@ -796,7 +774,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) bv[NCG * jj + cg] = Ub[(int64_t)jj * CI * CO + (4 * st) * CO + 16 * cg];
   };
-  float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
+  // EPI_BWD_UNPOOL writes the POOLED gradient [HO][WO][CO] of the layer below (its consumers un-pool it)
+  float* o = a.out + slot * ((POOL ? PH * PW : HO * WO) * CO);
   const float* bias = (EPI == EPI_FWD || POOL) ? a.bias + (int64_t)r * a.b_rstride : nullptr;
   const float* act = (EPI == EPI_BWD_MASK) ? a.aux + slot * (HO * WO * CO) : nullptr;
   const uint8_t* cd = (EPI == EPI_BWD_UNPOOL) ? a.code_in + slot * (HO * WO * CO) : nullptr;
@@ -812,15 +791,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int st = 0; st < KR; ++st) load_b(st, bw[st]);
   __syncthreads();
-  // The group loop, compiled once per wave (MPLC_ROW_WSPEC): B^T row i combines patch rows (ra, rb) with signs
-  // (sa, sb), t = sa*d[ra] + sb*d[rb]; with the wave's row a compile-time constant that is one add or subtract per
-  // value instead of a multiply and a multiply-add (the products by +-1 are exact: the same values either way)
+  // The group loop, compiled once per wave: B^T row i combines patch rows (ra, rb) with signs (+-1), t = sa d[ra] +
+  // sb d[rb]; with the wave's row a compile-time constant that is one add or subtract per value instead of a
+  // multiply and a multiply-add (the products by +-1 are exact: the same values either way; -2..-15 % per layer).
+  // Each copy contains the band's barriers: every wave takes exactly one copy and passes the same barriers in the
+  // same order and number as the others (s_barrier counts the workgroup's waves); the probes' v(S) hashes guard
+  // the equivalence with the runtime-sign form this replaced.
   auto groups = [&](auto wtag) __attribute__((always_inline)) {
   constexpr int WIC = decltype(wtag)::value;
-  const int ra = WIC >= 0 ? (WIC == 0 ? 0 : 1) : (wi == 0 ? 0 : 1);
-  const int rb = WIC >= 0 ? (WIC == 3 ? 3 : 2) : (wi == 3 ? 3 : 2);
-  const float sa = WIC >= 0 ? (WIC == 2 ? -1.0f : 1.0f) : (wi == 2 ? -1.0f : 1.0f);
-  const float sb = WIC >= 0 ? ((WIC == 0 || WIC == 3) ? -1.0f : 1.0f) : ((wi == 0 || wi == 3) ? -1.0f : 1.0f);
+  constexpr int ra = (WIC == 0) ? 0 : 1;
+  constexpr int rb = (WIC == 3) ? 3 : 2;
   const int drow = (rb - ra) * ROWP;
 #pragma unroll 1
   for (int g = 0; g < NG; ++g) {
@@ -840,12 +820,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float t[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if constexpr (WIC >= 0) {
-          const float da = d0[c * CIP], db = d0[drow + c * CIP];
-          t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
-        } else {
-          t[c] = sa * d0[c * CIP] + sb * d0[drow + c * CIP];
-        }
+        const float da = d0[c * CIP], db = d0[drow + c * CIP];
+        t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
       }
       float v[4];
       v[0] = t[0] - t[2];
@@ -950,15 +926,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
   };
-  if constexpr (MPLC_ROW_WSPEC) {
-    switch (wi) {  // wave-uniform
-      case 0: groups(IntC<0>{}); break;
-      case 1: groups(IntC<1>{}); break;
-      case 2: groups(IntC<2>{}); break;
-      default: groups(IntC<3>{}); break;
-    }
-  } else {
-    groups(IntC<-1>{});
+  switch (wi) {  // wave-uniform
+    case 0: groups(IntC<0>{}); break;
+    case 1: groups(IntC<1>{}); break;
+    case 2: groups(IntC<2>{}); break;
+    default: groups(IntC<3>{}); break;
   }
 
 }
@@ -1169,11 +1141,9 @@ void wgrad_kernel(const WgArgs a) {
 // half the LDS reads and 2/3 of the VALU per MFMA of the row-per-wave form at CO = 32 (which issues 8 MFMAs
 // per 8 reads and 12 adds).  NW waves per block = the band's 16-tile groups.
 // ------------------------------------------------------------------------------------------------
-#ifndef MPLC_WL_PRE_RR
-#define MPLC_WL_PRE_RR 4  // tile rows of the ReLU' operand loaded during the last k-step (0..4)
-#endif
 template <int HI, int WI, int CI, int CO, int PAD, int BTY, int NW, int EPI, int UPI = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_wl_kernel(const ConvArgs a) {
+  static_assert(EPI != EPI_BWD_UNPOOL, "the pooled-gradient epilogue (EPI_BWD_UNPOOL) is wino_kernel's");
   constexpr bool POOL = (EPI == EPI_FWD_POOL);
   constexpr int HO = HI + 2 * PAD - 2, WO = WI + 2 * PAD - 2;
   constexpr int PH = HO / 2, PW = WO / 2;
@@ -1193,7 +1163,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (j >= count) return;
   const int tid = threadIdx.x;
   const int64_t slot = (int64_t)r * a.bmax + j;
-  constexpr int IN_SZ = HI * WI * CI;
+  constexpr int IN_SZ = UPI ? (HI / 2) * (WI / 2) * CI : HI * WI * CI;  // UPI: a pooled gradient's slots
   const float* src = a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ : a.in + slot * IN_SZ;
   const int ty0 = band * BTY;
   const int bty = min(BTY, TYT - ty0);
@@ -1292,7 +1262,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // the last k-step, so that its latency is covered by that k-step's 32 MFMAs (all 4 rows: conv2's data gradient
   // -40 %, 2 registers spilled; 2 rows -25 %, 1 row -13 %; the peeled loop alone -4 %; bit-identical)
   constexpr bool PRE_MASK = (EPI == EPI_BWD_MASK);
-  constexpr int PRE_RR = MPLC_WL_PRE_RR;
+  constexpr int PRE_RR = 4;  // tile rows of the ReLU' operand loaded during the last k-step
   float mk[PRE_MASK && PRE_RR > 0 ? 8 * PRE_RR : 1];
   auto load_mask = [&]() {
     const float* ax = a.aux + slot * (HO * WO * CO);
@@ -1309,8 +1279,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
     }
   };
-  // EPI_FWD_POOL: the lane's two bias values likewise (MPLC_FWD_BIAS_PRE)
-  constexpr bool PRE_BIAS = POOL && MPLC_FWD_BIAS_PRE;
+  // EPI_FWD_POOL: the lane's two bias values likewise (conv2 forward -4 %)
+  constexpr bool PRE_BIAS = POOL;
   float bpre[2] = {0.0f, 0.0f};
   float b0[32], b1[32];
   load_b(0, b0);
@@ -1337,7 +1307,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   if constexpr (PRE_BIAS) asm volatile("" : "+v"(bpre[0]), "+v"(bpre[1]));
   // output transform in registers: lane holds M[xi][tile 4 kq + rr][co 16 cg + tl]
-  float* o = a.out + slot * ((EPI == EPI_BWD_UNPOOL ? 4 : 1) * (POOL ? PH * PW : HO * WO) * CO);
+  float* o = a.out + slot * ((POOL ? PH * PW : HO * WO) * CO);
   const uint32_t rseed = (POOL && a.drop_key) ? drop_row_seed(a.drop_key[r], a.drop_layer, (uint32_t)j) : 0u;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -1389,14 +1359,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const float av = rr < PRE_RR ? mk[((rr < PRE_RR ? rr : 0) * 2 + cg) * 4 + q]
                                          : a.aux[slot * (HO * WO * CO) + o_i];
             o[o_i] = av > 0.0f ? y[q] : 0.0f;
-          } else if constexpr (EPI == EPI_BWD_UNPOOL) {
-            const uint32_t c = a.code_in[slot * (HO * WO * CO) + o_i];
-            const float dv = (c & CODE_KEEP) ? y[q] * SCALE_25 : 0.0f;
-            const bool pos = (c & CODE_POS) != 0;
-            const int sel = c & 3;
-#pragma unroll
-            for (int p4 = 0; p4 < 4; ++p4)
-              o[((2 * yy + (p4 >> 1)) * (2 * WO) + 2 * xx + (p4 & 1)) * CO + co] = (pos && sel == p4) ? dv : 0.0f;
           } else {
             o[o_i] = fmaxf(y[q] + a.bias[(int64_t)r * a.b_rstride + co], 0.0f);
           }
@@ -1456,17 +1418,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fvec4 gb = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // db partial of channels 4 * (tid % (CO / 4)) .. + 3
-  // the sample loop compiled once per wave (MPLC_ROW_WSPEC, as in wino_kernel): the wave's transform row fixes the
-  // signs of B^T (sa, sb) and A (ai0, ai1), so V and D take adds / subtracts / moves instead of multiplies by 0 / +-1
+  // the sample loop compiled once per wave (as the group loop of wino_kernel, and with the same barrier argument):
+  // the wave's transform row fixes the signs of B^T and A, so V and D take adds / subtracts / moves instead of
+  // multiplies by 0 / +-1
   auto samples = [&](auto wtag) __attribute__((always_inline)) {
   constexpr int WIC = decltype(wtag)::value;
-  const int wv = WIC >= 0 ? WIC : wi;
-  const int ra = (wv == 0) ? 0 : 1;
-  const int rb = (wv == 3) ? 3 : 2;
-  const float sa = (wv == 2) ? -1.0f : 1.0f;
-  const float sb = (wv == 0 || wv == 3) ? -1.0f : 1.0f;
-  const float ai0 = (wv == 3) ? 0.0f : 1.0f;                       // A[i][0]
-  const float ai1 = (wv == 0) ? 0.0f : ((wv == 1) ? 1.0f : -1.0f);  // A[i][1]
+  constexpr int ra = (WIC == 0) ? 0 : 1;
+  constexpr int rb = (WIC == 3) ? 3 : 2;
   const int drow = (rb - ra) * XROW;
   // staging of (sample, band) in two halves: the global loads into registers, then the LDS images.  PIPE: the
   // next band's loads are issued right after this band's LDS stores, so that they land during this band's MFMAs
@@ -1485,7 +1443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto stage_load = [&](int jj, int bnd) {
     const int64_t sl = (int64_t)r * a.bmax + jj;
     const float* X = a.x + sl * (HI * WI * CI) + chn * CIB;
-    const float* Z = a.dz + sl * (HO * WO * CO);
+    const float* Z = a.dz + sl * (UPZ ? (HO / 2) * (WO / 2) * CO : HO * WO * CO);  // UPZ: pooled slots
     const int ty0 = bnd * BTY;
 #pragma unroll
     for (int k = 0; k < NITX; ++k) {  // input rows 2 ty0 - PAD .., columns -PAD .., the chunk's channels
@@ -1583,12 +1541,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           float t[4];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if constexpr (WIC >= 0) {
-              const float da = d0[c * CIP + 16 * h], db = d0[drow + c * CIP + 16 * h];
-              t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
-            } else {
-              t[c] = sa * d0[c * CIP + 16 * h] + sb * d0[drow + c * CIP + 16 * h];
-            }
+            const float da = d0[c * CIP + 16 * h], db = d0[drow + c * CIP + 16 * h];
+            t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
           }
           va[h][0] = ok ? t[0] - t[2] : 0.0f;
           va[h][1] = ok ? t[1] + t[2] : 0.0f;
@@ -1611,12 +1565,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           } else if constexpr (WIC == 2) {
             r0 = y00 - y10;
             r1 = y01 - y11;
-          } else if constexpr (WIC == 3) {
+          } else {
             r0 = -y10;
             r1 = -y11;
-          } else {
-            r0 = ai0 * y00 + ai1 * y10;
-            r1 = ai0 * y01 + ai1 * y11;
           }
           db[cg][0] = r0;
           db[cg][1] = r0 + r1;
@@ -1633,15 +1584,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
   };
-  if constexpr (MPLC_ROW_WSPEC) {
-    switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
-      case 0: samples(IntC<0>{}); break;
-      case 1: samples(IntC<1>{}); break;
-      case 2: samples(IntC<2>{}); break;
-      default: samples(IntC<3>{}); break;
-    }
-  } else {
-    samples(IntC<-1>{});
+  switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
+    case 0: samples(IntC<0>{}); break;
+    case 1: samples(IntC<1>{}); break;
+    case 2: samples(IntC<2>{}); break;
+    default: samples(IntC<3>{}); break;
   }
   // inverse transform dW[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]; lane holds
   // ci 16 h + 4 kq + rr (of the chunk), co 16 cg + tl
@@ -1710,11 +1657,8 @@ __global__ void rmsprop_small_kernel(const int32_t* __restrict__ cnt, const int3
 // Dense(512) + ReLU (+ dropout .5 when training): H[slot][n] = relu(sum_k D4[slot][k] W5[k][n] + b5[n]).
 // Block = 32 samples x 128 columns (4 waves x 32); A staged in LDS, W5 streamed.
 // ------------------------------------------------------------------------------------------------
-#ifndef MPLC_D5F_K
-#define MPLC_D5F_K 32  // dense5_fwd: rows of W5 per K chunk (the MFMA chain order is the same for any): 32 -2 % vs 64
-                       // (76 registers, more waves); 128 / 192 +6 % / +30 % (219 / 256 registers)
-#endif
-constexpr int DF_K = MPLC_D5F_K;
+constexpr int DF_K = 32;  // dense5_fwd: rows of W5 per K chunk (the MFMA chain order is the same for any): 32 -2 % vs
+                          // 64 (76 registers, more waves); 128 / 192 +6 % / +30 % (219 / 256 registers)
 static_assert(FEAT % DF_K == 0, "dense5_fwd K chunks");
 
 __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict__ A, const int32_t* __restrict__ cnt,
@@ -1925,14 +1869,8 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5,
 #define MPLC_D5_MFMA 1  // dense5_bwd_kernel (bit-identical MFMA form) instead of the VALU form
 #endif
 constexpr int D5_ROWS = 8;      // rows in flight (one per 32 threads)
-#ifndef MPLC_D5_GROUPS
-#define MPLC_D5_GROUPS 4
-#endif
-constexpr int D5_GROUPS = MPLC_D5_GROUPS;  // row groups per block
-#ifndef MPLC_D5_SCHUNK
-#define MPLC_D5_SCHUNK 16
-#endif
-constexpr int D5_SCHUNK = MPLC_D5_SCHUNK;  // samples staged at a time
+constexpr int D5_GROUPS = 4;   // row groups per block (1 / 2: -8 % .. +2.5 % on two probes, not kept)
+constexpr int D5_SCHUNK = 16;  // samples staged at a time (12: no gain)
 
 __global__ __launch_bounds__(256) void dense5_bwd_valu_kernel(
     const float* __restrict__ D4, const uint8_t* __restrict__ code4, const float* __restrict__ dH,
@@ -2333,9 +2271,13 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK, 1>   /* 8x8 tiles,    2 bands, 63.7 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 // Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
-#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1, MPLC_WG_PIPE>  /* 15x15 tiles, 5 bands, 56.9 KB */
+#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1, 0>  /* 15x15 tiles, 5 bands, 56.9 KB */
 #define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 57.1 KB */
-#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1, MPLC_WG_PIPE4>  /* 6x6 tiles, 1 band, 2 ci chunks */
+#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1, 1>  /* 6x6 tiles, 1 band, 2 ci chunks */
+// dz2 / dz4 slots hold the pooled gradients: conv3's data gradient (out [15][15][32]) and dense5_bwd write them,
+// conv2's / conv4's data (UPI: in [HI/2][WI/2][CI]) and weight (UPZ: dz [HO/2][WO/2][CO]) gradients read them
+static_assert(15 * 15 * 32 == MPLC_CIFAR_DZ2 && (30 / 2) * (30 / 2) * 32 == MPLC_CIFAR_DZ2, "dz2 slot stride");
+static_assert(6 * 6 * 64 == MPLC_CIFAR_DZ4 && (13 / 2) * (13 / 2) * 64 == MPLC_CIFAR_DZ4, "dz4 slot stride");
 
 inline int launch_status() {
   const hipError_t e = hipGetLastError();

@@ -60,7 +60,7 @@ SIGNATURES = {
                                c_void_p]),
 }
 
-ABI_VERSION = 2  # include/mplc_hip.h MPLC_ABI_VERSION
+ABI_VERSION = 3  # include/mplc_hip.h MPLC_ABI_VERSION
 
 
 def check_layout(query, expected, what):

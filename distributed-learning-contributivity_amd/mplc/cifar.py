@@ -18,7 +18,7 @@ STRIDE = 1251008
 NPARAM = 1250954
 WG_SAMPLES = 2
 A1, D2, A3, D4, H5 = 32768, 7200, 14400, 2304, 512
-DZ4, DZ3, DZ2, DZ1 = 10816, 14400, 28800, 32768
+DZ4, DZ3, DZ2, DZ1 = 2304, 14400, 7200, 32768  # dz4 / dz2: the pooled gradients (ABI 3)
 WT, WPART = 114688, 65664  # MPLC_CIFAR_WT: conv2..conv4 in Winograd form
 EVAL_FLOATS = A1 + D2 + A3 + D4 + H5  # per model per evaluated sample
 
@@ -124,7 +124,7 @@ class CifarModel:
             a1=torch.empty((R, B, A1), **f32), d2=torch.empty((R, B, D2), **f32), code2=torch.empty((R, B, D2), **u8),
             a3=torch.empty((R, B, A3), **f32), d4=torch.empty((R, B, D4), **f32), code4=torch.empty((R, B, D4), **u8),
             d5=torch.empty((R, B, H5), **f32), code5=torch.empty((R, B, H5), **u8), dh5=torch.empty((R, B, H5), **f32),
-            dz4=torch.zeros((R, B, DZ4), **f32), dz3=torch.empty((R, B, DZ3), **f32),
+            dz4=torch.empty((R, B, DZ4), **f32), dz3=torch.empty((R, B, DZ3), **f32),
             dz2=torch.empty((R, B, DZ2), **f32), dz1=torch.empty((R, B, DZ1), **f32),
             wt=torch.empty((R, WT), **f32), wpart=torch.empty((R, splits, WPART), **f32), w5src=torch.empty(R, **i32))
         t = CifarTrainT()
@@ -170,8 +170,8 @@ class CifarModel:
         convolutions' unit) and the HBM bytes of the two W5 kernels (csrc/cifar_cnn.hip):
           dense5_fwd: W5 read; per sample the d4 row read, the h5 row written with its code byte;
           dense5_bwd: W5 read and written, the RMSprop accumulator written (and read unless the optimizer is
-                      fresh, t = 1); per sample d4, its code byte and dh5 read, the un-pooled dz4 written (4
-                      window pixels per pooled element).
+                      fresh, t = 1); per sample d4, its code byte and dh5 read, the POOLED dz4 written (one
+                      float per pooled element since round 4; rounds 3-4 counted 4 window pixels, 1.5 % more).
         A FedAvg round's first step reads W5 from the coalition row (w5src >= 0), shared by the coalition's
         replicas: counted once per coalition."""
         import torch
@@ -184,7 +184,7 @@ class CifarModel:
             n_shared_rows = float(torch.unique(src[shared & (cnt > 0)]).numel())
             own = (~shared).to(torch.float64)
             acc_rd = (at > 1).to(torch.float64)
-            d5b += float((act * (w5 * (own + 2.0 + acc_rd)) + cnt * float(D4 * 4 + D4 + H5 * 4 + 4 * D4 * 4)).sum())
+            d5b += float((act * (w5 * (own + 2.0 + acc_rd)) + cnt * float(D4 * 4 + D4 + H5 * 4 + D4 * 4)).sum())
             d5f += float((act * w5 * own + cnt * float(D4 * 4 + H5 * 4 + H5)).sum())
             d5b += n_shared_rows * w5
             d5f += n_shared_rows * w5

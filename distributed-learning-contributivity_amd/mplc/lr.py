@@ -108,11 +108,12 @@ class LogRegEngine:
         _native.check(st, "mplc_lr_fedavg")
         scores = correct.cpu().numpy().astype(np.float64) / float(self.y_test_d.numel())
         self.last_theta = theta.cpu().numpy()
+        self.last_epochs_done = epochs_done.cpu().numpy().astype(np.int64)  # realised epochs (early stopping)
         self.stats["coalitions"] += C
         self.stats["batches"] += 1
         self.stats["replicas"] += sum(len(c) for c in coalitions)
         if return_details:
-            out = {"scores": scores, "epochs_done": epochs_done.cpu().numpy().astype(np.int64)}
+            out = {"scores": scores, "epochs_done": self.last_epochs_done}
             if return_models:  # Titanic.LogisticRegression.get_weights(): [coef | intercept], shape (1, 28)
                 out["models"] = [self.last_theta[ci].reshape(1, -1).copy() for ci in range(C)]
             if hist is not None:

@@ -150,12 +150,20 @@ class MultiPartnerLearning:
     def evaluate_coalitions(cls, scenario, coalitions):
         """Batched v(S) for many coalitions (test accuracy of the trained coalition model), float64 array.
         Under torch.distributed the coalitions are LPT-sharded over the ranks (mplc.parallel)."""
-        from .parallel import sharded_evaluate
+        from .parallel import EpochModel, sharded_evaluate
         eng = _engine(scenario)
 
         def local(cs):  # Contributivity always builds its learners with is_early_stopping=True
             return eng.evaluate(cs, is_early_stopping=True)
-        return sharded_evaluate(local, list(coalitions), eng.partner_sizes, eng.device)
+        # with early stopping a coalition's cost follows its realised epochs: the LPT plan learns them per size
+        es = bool(getattr(eng, "is_early_stopping", False)) and int(getattr(eng, "epoch_count", 0)) > constants.PATIENCE
+        model = None
+        if es:
+            model = getattr(eng, "epoch_model", None)
+            if model is None:
+                model = eng.epoch_model = EpochModel(eng.epoch_count)
+        return sharded_evaluate(local, list(coalitions), eng.partner_sizes, eng.device,
+                                epochs_local=(lambda: eng.last_epochs_done) if es else None, epoch_model=model)
 
 
 class SinglePartnerLearning(MultiPartnerLearning):

@@ -32,8 +32,9 @@ extern "C" {
 #define MPLC_E_SHAPE (-3)      /* tensor geometry the kernel does not support                    */
 
 /* Version / capability probe: returns MPLC_ABI_VERSION.  Version 2: the CIFAR10 Winograd weight workspace
- * (MPLC_CIFAR_WT 114688) and the layout queries mplc_cnn_layout / mplc_cifar_layout. */
-#define MPLC_ABI_VERSION 2
+ * (MPLC_CIFAR_WT 114688) and the layout queries mplc_cnn_layout / mplc_cifar_layout.  Version 3: the CIFAR10
+ * pooled-gradient slots dz4 / dz2 at their pooled sizes (MPLC_CIFAR_DZ4 2304, MPLC_CIFAR_DZ2 7200). */
+#define MPLC_ABI_VERSION 3
 int mplc_abi_version(void);
 
 /* ------------------------------------------------------------------------------------------------

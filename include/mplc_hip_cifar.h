@@ -54,9 +54,9 @@ extern "C" {
 #define MPLC_CIFAR_A3 14400          /* conv3 out 15x15x64 (ReLU)                 */
 #define MPLC_CIFAR_D4 2304           /* pool4 + dropout out 6x6x64 (= flatten)    */
 #define MPLC_CIFAR_H5 512            /* dense5 out (ReLU + dropout)               */
-#define MPLC_CIFAR_DZ4 10816         /* slot stride of dz4 (its pooled content: 6x6x64) */
+#define MPLC_CIFAR_DZ4 2304          /* slot stride of dz4: the pooled gradient 6x6x64 (ABI 3) */
 #define MPLC_CIFAR_DZ3 14400         /* conv3 pre-activation gradient 15x15x64    */
-#define MPLC_CIFAR_DZ2 28800         /* slot stride of dz2 (its pooled content: 15x15x32) */
+#define MPLC_CIFAR_DZ2 7200          /* slot stride of dz2: the pooled gradient 15x15x32 (ABI 3) */
 #define MPLC_CIFAR_DZ1 32768         /* conv1 pre-activation gradient 32x32x32    */
 #define MPLC_CIFAR_WT 114688         /* W2|W3|W4 in Winograd form (16 x ci x co each): the forward's, then
                                         the data gradients' (rotated, channels swapped) */
@@ -100,11 +100,11 @@ typedef struct {
   float* d5;              /* [.][MPLC_CIFAR_H5] dropout(relu(dense5))                     */
   uint8_t* code5;         /* [.][MPLC_CIFAR_H5] 0x40 kept | 0x80 positive                 */
   float* dh5;             /* [.][MPLC_CIFAR_H5]                                           */
-  float* dz4;             /* [.][MPLC_CIFAR_DZ4]: the POOLED dense5 input gradient [6][6][64] at  */
-                          /* the slot's start, un-pooled by conv4's gradient kernels (code4)   */
+  float* dz4;             /* [.][MPLC_CIFAR_DZ4]: the POOLED dense5 input gradient [6][6][64],  */
+                          /* un-pooled by conv4's gradient kernels (code4)                    */
   float* dz3;             /* [.][MPLC_CIFAR_DZ3]                                          */
-  float* dz2;             /* [.][MPLC_CIFAR_DZ2]: the POOLED conv3 input gradient [15][15][32] */
-                          /* at the slot's start, un-pooled by conv2's gradient kernels (code2) */
+  float* dz2;             /* [.][MPLC_CIFAR_DZ2]: the POOLED conv3 input gradient [15][15][32], */
+                          /* un-pooled by conv2's gradient kernels (code2)                    */
   float* dz1;             /* [.][MPLC_CIFAR_DZ1]                                          */
   float* wt;              /* [n_rep][MPLC_CIFAR_WT] Winograd-form conv weights (workspace)  */
   float* wpart;           /* [n_rep][wg_splits][MPLC_CIFAR_WPART]                         */

@@ -1,4 +1,4 @@
-"""Emulate rank 0 of an N-GPU config #4 TMCS run on a single GPU (record and replay).
+"""Emulate an N-GPU config #4 TMCS run on a single GPU (record and replay, every rank).
 
 An N-rank run plans TMCS waves N times longer (Contributivity._truncated_loop: mc_wave_scale = world size) and
 LPT-shards every frontier batch over the ranks (mplc.parallel.sharded_evaluate); the estimator itself runs
@@ -6,9 +6,9 @@ SPMD on every rank.  On one GPU:
   1. run the whole job with mc_wave_scale = N, recording every batch the estimator requested and the time
      spent training it (the rest of the wall time is host work every rank repeats: walks, planning, the
      stopping rule);
-  2. replay: train only rank 0's LPT share of each recorded batch (v(S) is a deterministic function of
-     (S, seed), so the shares are exactly the coalitions rank 0 would train), timed.
-rank 0's time ~ host time of 1. + training time of 2.  (The all_reduce of each batch's values - a few KB over
+  2. replay: train every rank's LPT share of each recorded batch (v(S) is a deterministic function of
+     (S, seed), so the shares are exactly the coalitions each rank would train), timed.
+job time ~ host time of 1. + the sum over batches of the slowest rank's training time in 2.  (The all_reduce of each batch's values - a few KB over
 xGMI - is not included.)
 python scripts/emulate_rank_mc.py N [method]"""
 import os
@@ -63,19 +63,27 @@ trained = sum(len(b) for b in batches)
 print(f"[{METHOD} N={N}] full job on 1 GPU: {wall:.1f} s ({train_s[0]:.1f} s training, {host:.1f} s host), "
       f"{len(batches)} batches, {trained} coalitions trained, {evals} evaluated by the estimator", flush=True)
 sizes = eng.partner_sizes
-rank0_train, rank0_reps = 0.0, 0
+# replay: every rank's LPT share of every batch, timed; the N-rank job waits at each batch's all_reduce for its
+# slowest rank, so its training time is the sum over batches of the max over ranks
+per_rank = np.zeros(N)
+synced, reps = 0.0, np.zeros(N)
 for b in batches:
-    shard = parallel.lpt_shard([parallel.coalition_cost(k, sizes) for k in b], N)[0]
-    if not shard:
-        continue
-    mine = [b[i] for i in shard]
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    eng.evaluate(mine, is_early_stopping=True)
-    torch.cuda.synchronize()
-    rank0_train += time.perf_counter() - t1
-    rank0_reps += sum(len(k) for k in mine)
-rank0 = host + rank0_train
-print(f"[{METHOD} N={N}] emulated rank 0: {rank0:.1f} s ({rank0_train:.1f} s training {rank0_reps} replicas in "
-      f"{len(batches)} batches = {rank0_reps / max(1, len(batches)):.0f} per batch, {host:.1f} s host) -> "
-      f"whole-job value {evals / rank0:.2f} evals/s", flush=True)
+    shards = parallel.lpt_shard([parallel.coalition_cost(k, sizes) for k in b], N)
+    times = np.zeros(N)
+    for r, shard in enumerate(shards):
+        if not shard:
+            continue
+        mine = [b[i] for i in shard]
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.evaluate(mine)
+        torch.cuda.synchronize()
+        times[r] = time.perf_counter() - t1
+        reps[r] += sum(len(k) for k in mine)
+    per_rank += times
+    synced += times.max()
+job = host + synced
+print(f"[{METHOD} N={N}] emulated job: {job:.1f} s = host {host:.1f} s + sum over batches of the slowest rank's "
+      f"training {synced:.1f} s (ranks' own totals {np.round(per_rank, 1).tolist()}, replicas per rank "
+      f"{reps.astype(int).tolist()}, {reps.mean() / max(1, len(batches)):.0f} per batch) -> whole-job value "
+      f"{evals / job:.2f} evals/s", flush=True)

@@ -56,10 +56,13 @@ def test_argument_errors_without_gpu():
 
 
 def test_abi_version_bumped_with_the_cifar_layout():
-    # version 2: MPLC_CIFAR_WT grew to 114688 (Winograd weights) and the layout queries were added
-    assert _native.ABI_VERSION == 2
+    # version 2: MPLC_CIFAR_WT grew to 114688 (Winograd weights) and the layout queries were added; version 3: the
+    # pooled-gradient slots dz4 / dz2 shrank to their pooled sizes
+    assert _native.ABI_VERSION == 3
     text = open(os.path.join(REPO, "include", "mplc_hip.h")).read()
-    assert re.search(r"#define MPLC_ABI_VERSION 2\b", text)
+    assert re.search(r"#define MPLC_ABI_VERSION 3\b", text)
+    defs = _header_defines("mplc_hip_cifar.h")
+    assert (defs["MPLC_CIFAR_DZ4"], defs["MPLC_CIFAR_DZ2"]) == (6 * 6 * 64, 15 * 15 * 32)
 
 
 def _header_defines(name):

@@ -100,6 +100,26 @@ def _worker(rank, world, port, out_q):
         c = Contributivity(scenario=sc)
         c.compute_contributivity(method)
         results[method] = (c.contributivity_scores.tolist(), c.scores_std.tolist(), c.first_charac_fct_calls_count)
+    # early stopping: realised epochs (here a fixed function of the coalition) travel with the values and weight the
+    # LPT costs; every rank must hold the same epoch model and the estimates must not change
+    from mplc.parallel import EpochModel
+    last = []
+    model = EpochModel(40)
+
+    def local_es(coals):
+        last[:] = [15 + (sum((i + 1) * (i + 3) for i in c) % 14) for c in coals]
+        return local(coals)
+
+    class ApproachES:
+        @staticmethod
+        def evaluate_coalitions(scenario, cs):
+            return sharded_evaluate(local_es, list(cs), sizes, epochs_local=lambda: list(last), epoch_model=model)
+    sc_es = types.SimpleNamespace(partners_list=partners, multi_partner_learning_approach=ApproachES)
+    np.random.seed(7)
+    c = Contributivity(scenario=sc_es)
+    c.compute_contributivity("TMCS")
+    results["TMCS_es"] = (c.contributivity_scores.tolist(), c.scores_std.tolist(), c.first_charac_fct_calls_count)
+    results["epoch_model"] = (sorted(model.sum.items()), sorted(model.cnt.items()))
     out_q.put((rank, mine, results))
     dist.barrier()
     dist.destroy_process_group()
@@ -128,3 +148,21 @@ def test_two_rank_sharded_evaluation_and_spmd_estimator(monkeypatch):
         scores, std, calls = res[0][2][method]
         assert scores == ref.contributivity_scores.tolist() and std == ref.scores_std.tolist(), method
         assert calls == ref.first_charac_fct_calls_count, method
+    # the epoch-weighted plan changes no result, and both ranks learned the same epoch model from the all_reduce
+    assert res[0][2]["TMCS_es"] == res[0][2]["TMCS"]
+    assert res[0][2]["epoch_model"][1] and res[0][2]["epoch_model"] == res[1][2]["epoch_model"]
+
+
+def test_epoch_model_weights_lpt_costs():
+    """EpochModel: per-size mean once MIN_SEEN coalitions of a size are known, else the overall mean, else the
+    configured epochs; the LPT costs scale with it (a size that trains twice as long weighs twice as much)."""
+    from mplc.parallel import EpochModel, coalition_cost
+    m = EpochModel(40)
+    assert m.predict(3) == 40.0
+    m.update([(0,), (1,), (2,), (3,)], [10, 10, 10, 10])
+    m.update([(0, 1)], [30])
+    assert m.predict(1) == 10.0 and m.predict(2) == 14.0  # size 2 seen once: the overall mean (70 / 5)
+    sizes = [100, 100, 100, 100]
+    assert coalition_cost((0, 1), sizes, m.predict(2)) == 200 * 14.0
+    costs = [coalition_cost(c, sizes, e) for c, e in (((0,), 28.0), ((1,), 14.0), ((2,), 14.0))]
+    assert sorted(map(sorted, lpt_shard(costs, 2))) == [[0], [1, 2]]
