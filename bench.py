@@ -120,18 +120,28 @@ def host_threads():
     return max(1, n)
 
 
+PMC_FILES = ("pmc_traffic.json", "pmc_traffic_config4.json")  # config #3 (+ #5), config #4
+
+
+def pmc_entry(kernel, workload):
+    """The committed PMC record of `kernel` for the bench command of `workload` (profiles/pmc_traffic*.json, written
+    by scripts/pmc_traffic.py): bytes per launch, and for config #4 the algorithmic bytes of the same launches."""
+    for name in PMC_FILES:
+        try:
+            with open(os.path.join(REPO, "profiles", name)) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("workload") == workload and kernel in doc.get("kernels", {}):
+            return doc["kernels"][kernel]
+    return None
+
+
 def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the committed PMC passes of this same bench command
-    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py); None when absent or for another workload."""
-    try:
-        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
-            doc = json.load(f)
-    except (OSError, ValueError):
-        return None
-    e = doc.get("kernels", {}).get(kernel)
-    if e is None or doc.get("workload") != workload:
-        return None
-    return int(e["traffic_bytes_per_launch"])
+    """HBM bytes per launch of `kernel` from the committed PMC passes of this same bench command; None when absent
+    or for another workload."""
+    e = pmc_entry(kernel, workload)
+    return None if e is None else int(e["traffic_bytes_per_launch"])
 
 
 def _free_port():
@@ -694,8 +704,10 @@ def bench_cifar(args, rank, world, sub=False):
     from mplc.cifar import DIRECT_FLOP_PER_SAMPLE, FLOP_PER_SAMPLE
     from mplc.contributivity import Contributivity
     from mplc.engine import CoalitionEngine
-    from mplc.profiling import KernelTimer
+    from mplc.profiling import KernelTimer, StashOnly
     sc = build_cifar_scenario(args.cifar_epochs, args.signal, args.cifar_partners)
+    if args.mc_plan_overhead is not None:  # planner experiments: the speculation budget (mplc.mc.plan_frontier)
+        sc.mc_plan_overhead = args.mc_plan_overhead
     sc.engine = CoalitionEngine.for_scenario(sc)
     eng = sc.engine
     eng.warmup()
@@ -731,9 +743,13 @@ def bench_cifar(args, rank, world, sub=False):
         c.compute_contributivity(args.method)
         return c
 
+    # under rocprofv3 --pmc (no HIP events): every step's schedule stashed, so that the counters' bytes of ALL
+    # launches can be set beside the algorithmic bytes of the same launches (scripts/pmc_traffic.py)
+    stash_all = StashOnly(args.cifar_profile_kernel) if args.no_kernel_timer else None
+
     def timed_step(i, planned):
         if s0[0] == 0:
-            eng.profiler = None  # set per lockstep batch by progress()
+            eng.profiler = stash_all  # None: set per lockstep batch by progress()
             eng.time_test_eval = True
             s0[0] = eng.stats["samples"] or -1
         return one_step()
@@ -747,6 +763,13 @@ def bench_cifar(args, rank, world, sub=False):
     units = eng.model_impl.algorithmic_units(timer.stash)
     timer.stash = []
     kernels = cifar_kernel_table(timer, units) if not args.no_kernel_timer else {}
+    algorithmic_all = None
+    if stash_all is not None and stash_all.stash:
+        ua = eng.model_impl.algorithmic_units(stash_all.stash)
+        n_all = len(stash_all.stash)  # one launch of every training kernel per step
+        algorithmic_all = {"launches": n_all, "samples_per_launch": ua["samples"] / n_all,
+                           **{k.replace("_bytes", "_kernel"): v / n_all for k, v in ua.items() if k.endswith("_bytes")}}
+        stash_all.stash = []
     kern_ms = timer.total_ms(args.cifar_profile_kernel)
     launches = timer.launches(args.cifar_profile_kernel)
     samples = eng.stats["samples"] - max(0, s0[0])
@@ -799,6 +822,7 @@ def bench_cifar(args, rank, world, sub=False):
                              "kernel time; direct_equivalent_tflops prices the same time at the direct "
                              "convolution's count"},
         "kernels": kernels,
+        "algorithmic_bytes_per_launch_all": algorithmic_all,
         "kernel_timer": {"batches_timed": sampled["timed"], "batches": sampled["batches"],
                          "replica_steps_timed": sampled["timed_replica_steps"],
                          "replica_steps": sampled["replica_steps"],
@@ -809,9 +833,21 @@ def bench_cifar(args, rank, world, sub=False):
     dom = max((k for k in kernels if "frac" in kernels[k]), key=lambda k: kernels[k]["ms_total"], default=None)
     if dom is not None:
         kd = kernels[dom]
+        wl = out["config"]["workload"]
+        for k, e in kernels.items():  # PMC bytes per launch (all launches of the profiled run) beside the table
+            pe = pmc_entry(f"{k}_kernel", wl) if e.get("bound") == "hbm" else None
+            if pe is not None:
+                e["traffic_pmc"] = int(pe["traffic_bytes_per_launch"])
+                if pe.get("algorithmic_bytes_per_launch"):
+                    e["traffic_over_algorithmic"] = round(pe["traffic_bytes_per_launch"] / pe["algorithmic_bytes_per_launch"], 4)
         out["roofline_conv2_fwd"] = out["roofline"]
         out["roofline"] = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
-                           "frac": kd["frac"], "traffic": None, "kernel": dom, "launches": kd["launches"],
+                           "frac": kd["frac"], "traffic": kd.get("traffic_pmc"),
+                           "traffic_over_algorithmic": kd.get("traffic_over_algorithmic"),
+                           "traffic_source": "profiles/pmc_traffic_config4.json: FETCH_SIZE x2 + WRITE_SIZE per launch "
+                                             "over all launches of a --pmc run of this leg, beside the algorithmic bytes "
+                                             "of the same launches" if kd.get("traffic_pmc") else None,
+                           "kernel": dom, "launches": kd["launches"],
                            "kernel_ms_avg": kd["ms_avg"], "time_share": kd["time_share"],
                            "units_per_launch": kd["units_per_launch"],
                            "note": "the step's dominant kernel; achieved = " + kd["algorithmic"] +
@@ -928,6 +964,8 @@ def main():
     ap.add_argument("--compact-share", type=float, default=None,
                     help="train leg: early-stopping batch compaction threshold (default mplc/cnn.py; 0 = off)")
     ap.add_argument("--dump-values", default=None, help="cifar leg: save the trained v(S) values (npz) here")
+    ap.add_argument("--mc-plan-overhead", type=float, default=None,
+                    help="cifar leg: TMCS speculation budget in replica-trainings per batch (default: the library's 8)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events in the stream (rocprofv3 --pmc passes: counters only)")
     args = ap.parse_args()

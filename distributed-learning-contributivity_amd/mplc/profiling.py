@@ -96,3 +96,21 @@ class KernelTimer:
     def launches(self, name=None):
         self._fold(block=True)
         return self.count[name or self.kernel]
+
+
+class StashOnly:
+    """A profiler that times nothing and only stashes every step's schedule (bench.py under rocprofv3 --pmc, where
+    no HIP event may be recorded): the algorithmic units of ALL launches of the run, to set beside the counters'
+    bytes of the same launches."""
+    all = False
+    want_stash = True
+
+    def __init__(self, kernel):
+        self.kernel = kernel  # any kernel of the model: the library records nothing (NULL events)
+        self.stash = []
+
+    def pair(self):
+        return None, None
+
+    def stash_step(self, *tensors):
+        self.stash.append(tuple(t.clone() for t in tensors))

@@ -10,7 +10,7 @@ SPMD on every rank.  On one GPU:
      (S, seed), so the shares are exactly the coalitions each rank would train), timed.
 job time ~ host time of 1. + the sum over batches of the slowest rank's training time in 2.  (The all_reduce of each batch's values - a few KB over
 xGMI - is not included.)
-python scripts/emulate_rank_mc.py N [method]"""
+python scripts/emulate_rank_mc.py N [method] [mc_plan_overhead]"""
 import os
 import sys
 import time
@@ -18,18 +18,32 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "distributed-learning-contributivity_amd"))
+import threading
+
 import numpy as np
 import torch
 
 import bench
+
+_T0 = time.time()
+
+
+def _heartbeat():  # a line on stderr every 30 s: a long shard is not a hung GPU command
+    while True:
+        time.sleep(30)
+        print(f"heartbeat {time.time() - _T0:.0f}s", file=sys.stderr, flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 from mplc import parallel
 
 N = int(sys.argv[1])
 METHOD = sys.argv[2] if len(sys.argv) > 2 else "TMCS"
+OVERHEAD = float(sys.argv[3]) if len(sys.argv) > 3 else None  # planner speculation budget (mc_plan_overhead)
 batches, train_s = [], [0.0]
 
 
-def recording(evaluate_local, coalitions, partner_sizes, device=None):
+def recording(evaluate_local, coalitions, partner_sizes, device=None, **_):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     vals = np.asarray(evaluate_local(coalitions), dtype=np.float64)
@@ -43,6 +57,8 @@ parallel.sharded_evaluate = recording
 torch.cuda.set_device(0)
 sc = bench.build_cifar_scenario(1, 0.4)
 sc.mc_wave_scale = N
+if OVERHEAD is not None:
+    sc.mc_plan_overhead = OVERHEAD
 from mplc.contributivity import Contributivity
 from mplc.engine import CoalitionEngine
 sc.engine = CoalitionEngine.for_scenario(sc)

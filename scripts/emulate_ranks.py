@@ -16,6 +16,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "distributed-learning-contributivity_amd"))
+import threading  # noqa: E402
 from itertools import combinations  # noqa: E402
 
 import numpy as np  # noqa: E402
@@ -23,6 +24,17 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from mplc import parallel  # noqa: E402
+
+_T0 = time.time()
+
+
+def _heartbeat():  # a line on stderr every 30 s: a long shard is not a hung GPU command
+    while True:
+        time.sleep(30)
+        print(f"heartbeat {time.time() - _T0:.0f}s", file=sys.stderr, flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 
 
 def main():

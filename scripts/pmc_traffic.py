@@ -2,7 +2,9 @@
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 tallies wide coalesced reads at half their bytes, so FETCH is
 doubled; WRITE is taken as reported.  Usage: python scripts/pmc_traffic.py <fetch dir> <write dir> <bench json of the profiled run> <out.json>
-bench.py fills roofline.traffic from <out.json> when its workload string matches the profiled run's.
+bench.py fills roofline.traffic from <out.json> when its workload string matches the profiled run's
+(profiles/pmc_traffic.json: config #3 + #5; profiles/pmc_traffic_config4.json: the CIFAR10 leg, with the
+algorithmic bytes of the same launches when the profiled bench line carries them).
 """
 import csv
 import glob
@@ -34,9 +36,16 @@ def main(fetch_dir, write_dir, bench_json, out):
         res[k] = {"launches": launches, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "traffic_bytes_per_launch": rd + wr,
                   "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads) + WRITE_SIZE, KiB->bytes"}
-    line = [ln for ln in open(bench_json) if ln.startswith("{")][-1]
-    doc = {"workload": json.loads(line)["config"]["workload"], "source": f"{fetch_dir} + {write_dir}",
-           "kernels": res}
+    line = json.loads([ln for ln in open(bench_json) if ln.startswith("{")][-1])
+    # config #4 leg under --no-kernel-timer: the algorithmic bytes of ALL its launches (bench.py StashOnly), so the
+    # counters' bytes and the algorithm's bytes describe the same launches
+    alg = line.get("algorithmic_bytes_per_launch_all") or {}
+    for k, e in res.items():
+        if alg.get(k):
+            e["algorithmic_bytes_per_launch"] = alg[k]
+            e["traffic_over_algorithmic"] = e["traffic_bytes_per_launch"] / alg[k]
+            e["launches_stashed"] = alg["launches"]
+    doc = {"workload": line["config"]["workload"], "source": f"{fetch_dir} + {write_dir}", "kernels": res}
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
