@@ -963,12 +963,6 @@ constexpr int BWD_PAIRS = BWD_WR * PL * 16;    // (dp, code) pairs of a quarter
 constexpr int BWD_PRE = (BWD_PAIRS + BWD_THREADS - 1) / BWD_THREADS;
 constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quarter [co 16][ci 32][xi 16]
 constexpr int BWD_NIT = (IMG * IMG + BWD_THREADS - 1) / BWD_THREADS;  // image values per thread
-#ifndef BWD_UNPOOL2
-#define BWD_UNPOOL2 1
-#endif
-#ifndef BWD_W1PRE
-#define BWD_W1PRE 1
-#endif
 constexpr int BWD_SPB = 1;  // samples per block (9: +2 % on the probe, the sample loop spills 13 registers)
 static_assert(BWD_BANDS * BWD_BAND_TILES >= BWD_TILES && (BWD_BANDS - 1) * BWD_BAND_TILES < BWD_TILES,
               "MPLC_CNN_W1_BANDS must be ceil(169 / 64)");
@@ -1025,12 +1019,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   };
   fetch(j_begin, 0);
   load_img(j_begin);
-#if BWD_UNPOOL2
-  // the whole band zeroed once: a window's 4 pixels then stay zero but for its argmax pixel, which the window's
-  // owner thread (the same thread for every quarter and sample) clears and rewrites
-  for (int e = tid; e < BWD_DR * BWD_RS; e += BWD_THREADS) dz_s[e] = 0.0f;
-  uint32_t selp = 0;  // per pair s of this thread: the argmax pixel written last (2 bits each)
-#else
   {
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
@@ -1038,28 +1026,12 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       dz_s[(rr * BWD_DC + (c < 2 ? c : BWD_DC - 4 + c)) * BWD_CS + k] = 0.0f;
     }
   }
-#endif
   // A operand (V): this lane's tile tl of the wave's group at channel kq of each k-step
   const int tcl = min(gt0 + tl, BWD_TILES - 1);
   const int pa = ((2 * (tcl / 13 - ty0)) * BWD_DC + 2 * (tcl % 13)) * BWD_CS + kq;
   // B operand (Ur): ci = 16h + tl, co = 4st + kq of the quarter; chunk m of the 16 transform points at
   // m ^ swz (the staging applies the same XOR)
   const int swz = (tl >> 2) & 3;
-  // conv1 weights as the B operand of the epilogue's 16x16x4 recompute: W1e[4s + kq][16h + tl], rows 0..8 = taps,
-  // 9 = bias
-  auto load_w1b = [&](float (&w)[3][2]) {
-#pragma unroll
-    for (int s3 = 0; s3 < 3; ++s3)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = 4 * s3 + kq, ci = 16 * h + tl;
-        w[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
-      }
-  };
-#if BWD_W1PRE
-  float w1b[3][2];  // loaded up front: their latency hides behind the first quarter instead of the epilogue's start
-  load_w1b(w1b);
-#endif
 #pragma unroll 1
   for (int j = j_begin; j < j_end; ++j) {
   // img_s is free: the previous sample's epilogue reads end before its reduction barrier
@@ -1092,13 +1064,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           const float v = (c & 0x80) ? pdv[s] : 0.0f;
           const int sel = c & 3;
           float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
-#if BWD_UNPOOL2
-          // the previous argmax pixel cleared, the value written at this one (same thread: in order)
-          const uint32_t old = (selp >> (2 * s)) & 3u;
-          d[(old >> 1) * (BWD_DC * BWD_CS) + (old & 1) * BWD_CS] = 0.0f;
-          d[(sel >> 1) * (BWD_DC * BWD_CS) + (sel & 1) * BWD_CS] = v;
-          selp = (selp & ~(3u << (2 * s))) | ((uint32_t)sel << (2 * s));
-#else
           // the window's 4 pixels zeroed, then the value at the argmax (same thread, same address: in order): no
           // per-pixel compare / select chain (SGPR-mask hazards padded with s_nop in every one)
           d[0] = 0.0f;
@@ -1106,7 +1071,6 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           d[BWD_DC * BWD_CS] = 0.0f;
           d[BWD_DC * BWD_CS + BWD_CS] = 0.0f;
           d[(sel >> 1) * (BWD_DC * BWD_CS) + (sel & 1) * BWD_CS] = v;
-#endif
         }
       }
 #endif
@@ -1195,10 +1159,15 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   }
   // ---- epilogue (wave-local).  Lane (tl, kq) holds M[xi][tile 4kq + rr][ci 16h + tl] in acc[xi][h][rr].
   if (j + 1 < j_end) load_img(j + 1);  // in flight during the epilogue
-#if !BWD_W1PRE
+  // conv1 weights as the B operand of the 16x16x4 recompute: W1e[4s + kq][16h + tl], rows 0..8 = taps, 9 = bias
   float w1b[3][2];
-  load_w1b(w1b);
-#endif
+#pragma unroll
+  for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 4 * s3 + kq, ci = 16 * h + tl;
+      w1b[s3][h] = (k < 9) ? P[OFF_W1 + k * C1 + ci] : ((k == 9) ? P[OFF_B1 + ci] : 0.0f);
+    }
   fvec4 gacc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // [dW1 | db1] partial: rows = tap 4kq + reg, col = ci 16h + tl
   fvec4 gacc1 = gacc;
 #ifdef BWD_EXP_NOEPI  // timing experiment: the epilogue compiled out (the accumulators still consumed)

@@ -6,8 +6,9 @@ train as ONE lockstep batch.  Checks:
   - efficiency: sum of the Shapley values = v(N) (to 1e-12; v(empty) = 0, mplc/contributivity.py:1210-1253);
   - batch invariance: coalitions re-evaluated alone give bit-identical values to the 5120-replica batch;
   - |S| in {1, 2} coalitions against the oracle (oracle/cnn.py, sequential like the reference): no bias
-    (the mean SIGNED difference over eighteen coalitions - all ten singletons, eight pairs - within 1 pt),
-    mean |difference| within 2 pt, each within 4 pt (10000 test samples: 1 pt = 100 samples).  One epoch leaves the models in the steep part of
+    (the mean SIGNED difference over eighteen coalitions - all ten singletons, eight pairs - within 1 pt of the
+    oracle's median), each within the oracle's own spread over eight CPU thread counts widened by 1 pt (10000 test
+    samples: 1 pt = 100 samples).  One epoch leaves the models in the steep part of
     learning, where fp32 summation order alone moves a single coalition's accuracy by points: the oracle
     against ITSELF, run with 8 vs 3 CPU threads, gives 0.9675 vs 0.9793 for (0, 9), and 0.8766 (8 threads
     here) vs 0.8632 (16 threads on the GPU box) for (2, 7) at signal 0.2 (0.2-0.8 pt apart even at E=2),
@@ -70,22 +71,27 @@ def test_config3_batch_invariance(mnist10, config3_sweep):
 
 
 def test_config3_small_coalitions_vs_oracle(mnist10, config3_sweep):
-    from oracle import cnn as ocnn
+    """All ten singletons and eight pairs against the oracle's own spread over fp32 summation orders: the oracle at
+    1, 2, 3, 4, 6, 8, 12 and 16 CPU threads (tests/golden/oracle_spread_config3.json, scripts/oracle_spread.py) plus
+    one live run at the box's thread count.  After one epoch these models sit in the steep part of learning, where
+    the summation order alone moves a coalition by up to 4 pt in the oracle itself (e.g. (0, 9): 0.858 .. 0.900 over
+    the thread counts), so a bound against ONE oracle run had to be 2 pt mean |diff| / 4 pt max (rounds 2-4).  The
+    gate now: each coalition within the spread widened by 1 pt, and the mean signed difference to
+    the oracle's median within 1 pt."""
+    import torch
+    from spread_fixtures import load_spread, oracle_values
     c, eng = config3_sweep
-    ds = mnist10.dataset
-    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    prow = [p.train_idx for p in mnist10.partners_list]
-    bs = [p.batch_size for p in mnist10.partners_list]
-    # every singleton and eight pairs: a single coalition moves by up to ~4 pt with the fp32 summation order
-    # alone (module docstring), so the bias bound needs the larger sample (se of the mean ~0.4 pt here;
-    # profiles/r02_parity_probe_wg8_wg9.txt: mean signed difference -0.44 / +0.15 pt for two summation orders
-    # of conv2's weight gradient, while six coalitions alone gave -0.57 / +1.19 pt)
-    coals = [(p,) for p in range(10)] + [(2, 7), (0, 9), (4, 5), (1, 3), (6, 8), (0, 5), (2, 9), (3, 7)]
-    ref = np.array([ocnn.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=1, M=20)[0] for k in coals])
+    rec = load_spread("config3", mnist10)
+    coals = [tuple(k) for k in rec["coalitions"]]
+    refs = [rec["fp32"][str(t)] for t in rec["threads"]]
+    refs.append(oracle_values(mnist10, coals, torch.get_num_threads()))  # the box's own summation order
+    refs = np.array(refs)
     dev = np.array([c.charac_fct_values[k] for k in coals])
-    diff = dev - ref
-    assert abs(np.mean(diff)) <= 0.01, (dev, ref)                                  # no systematic bias
-    assert np.mean(np.abs(diff)) <= 0.02 and np.max(np.abs(diff)) <= 0.04, (dev, ref)
+    lo, hi = refs.min(axis=0) - 0.01, refs.max(axis=0) + 0.01
+    med = np.median(refs, axis=0)
+    print(list(zip(coals, dev.tolist(), refs.min(axis=0).tolist(), refs.max(axis=0).tolist(), rec["fp64"])))
+    assert abs(np.mean(dev - med)) <= 0.01, (dev, med)  # no systematic bias
+    assert np.all((lo <= dev) & (dev <= hi)), (coals, dev, refs)
 
 
 # ------------------------------------------------------------------------------------------------
