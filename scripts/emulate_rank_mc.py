@@ -10,7 +10,7 @@ SPMD on every rank.  On one GPU:
      (S, seed), so the shares are exactly the coalitions each rank would train), timed.
 job time ~ host time of 1. + the sum over batches of the slowest rank's training time in 2.  (The all_reduce of each batch's values - a few KB over
 xGMI - is not included.)
-python scripts/emulate_rank_mc.py N [method] [mc_plan_overhead]"""
+python scripts/emulate_rank_mc.py N [method] [mc_plan_overhead|-] [mc_wave_scale]"""
 import os
 import sys
 import time
@@ -39,7 +39,8 @@ from mplc import parallel
 
 N = int(sys.argv[1])
 METHOD = sys.argv[2] if len(sys.argv) > 2 else "TMCS"
-OVERHEAD = float(sys.argv[3]) if len(sys.argv) > 3 else None  # planner speculation budget (mc_plan_overhead)
+OVERHEAD = float(sys.argv[3]) if len(sys.argv) > 3 and sys.argv[3] != "-" else None  # mc_plan_overhead
+WAVE = int(sys.argv[4]) if len(sys.argv) > 4 else N  # mc_wave_scale (the product uses the world size)
 batches, train_s = [], [0.0]
 
 
@@ -56,7 +57,7 @@ def recording(evaluate_local, coalitions, partner_sizes, device=None, **_):
 parallel.sharded_evaluate = recording
 torch.cuda.set_device(0)
 sc = bench.build_cifar_scenario(1, 0.4)
-sc.mc_wave_scale = N
+sc.mc_wave_scale = WAVE
 if OVERHEAD is not None:
     sc.mc_plan_overhead = OVERHEAD
 from mplc.contributivity import Contributivity
@@ -76,7 +77,7 @@ wall = time.perf_counter() - t0
 host = wall - train_s[0]
 evals = c.first_charac_fct_calls_count
 trained = sum(len(b) for b in batches)
-print(f"[{METHOD} N={N}] full job on 1 GPU: {wall:.1f} s ({train_s[0]:.1f} s training, {host:.1f} s host), "
+print(f"[{METHOD} N={N} overhead={OVERHEAD} wave_scale={WAVE}] full job on 1 GPU: {wall:.1f} s ({train_s[0]:.1f} s training, {host:.1f} s host), "
       f"{len(batches)} batches, {trained} coalitions trained, {evals} evaluated by the estimator", flush=True)
 sizes = eng.partner_sizes
 # replay: every rank's LPT share of every batch, timed; the N-rank job waits at each batch's all_reduce for its
