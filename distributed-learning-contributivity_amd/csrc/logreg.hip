@@ -10,7 +10,14 @@
 //   score   accuracy of predict() = [w.x + b > 0] on the test set
 // One workgroup = one coalition; every fit is solved EXACTLY (damped Newton in fp64, gradient < 1e-10),
 // the optimum of the strictly convex problem sklearn approximates to tol 1e-4.
-// Work is tiny (28 unknowns, tens of rows): latency-bound; the point is doing all coalitions in ONE launch.
+// Work is tiny (28 unknowns, tens of rows): latency-bound; the point is doing all coalitions in ONE launch and
+// keeping each fit's dependent chain short.  Round 5: one wave per coalition (reductions in registers, no block
+// barriers), the fit's rows staged in LDS once per fit (the Newton iterations read them from LDS instead of
+// re-gathering them through the keyed permutation from global memory), the Hessian's entries spread over the
+// lanes, the Cholesky factorisation and the two triangular solves parallel over the rows (a single lane did them
+// serially: 28^3/6 dependent LDS round trips per iteration), and the line search's accepted objective reused as
+// the next iteration's start value.  The 1023-coalition sweep (config #2): 242 ms -> 40.3 ms
+// (profiles/r05_titanic_kernel_stats{,_onewave}.csv).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "keyed.h"
@@ -18,36 +25,40 @@
 
 namespace {
 
-constexpr int LR_THREADS = 256;
-constexpr int LR_MAXF = 64;   // features (+1 intercept) supported
-constexpr int LR_MAXP = 64;   // partners per coalition
-constexpr int LR_CHUNK = 2048; // rows whose sigma is staged in LDS at a time
+constexpr int LR_THREADS = 64;   // one wave per coalition
+constexpr int LR_MAXF = 32;      // D = n_features + 1 unknowns (coef | intercept) supported
+constexpr int LR_MAXP = 64;      // partners per coalition
+constexpr int LR_NMAX = 128;     // rows staged in LDS at a time (a whole Titanic fit: <= 71 rows)
+constexpr int LR_NE = LR_MAXF * (LR_MAXF + 1) / 2 + LR_MAXF;  // Hessian upper triangle + gradient entries
+constexpr int LR_EPL = (LR_NE + LR_THREADS - 1) / LR_THREADS;  // entries per lane
 
 struct Shared {
   double theta[LR_MAXF];
   double w[LR_MAXF];       // current Newton iterate
-  double g[LR_MAXF];
-  double d[LR_MAXF];
-  double H[LR_MAXF * LR_MAXF];
-  double acc[LR_MAXF];      // FedAvg accumulator
-  double red[LR_THREADS];
-  double sg[LR_CHUNK];      // sigma(-y z) of the staged rows
-  int rid[LR_CHUNK];        // their dataset row ids
+  double trial[LR_MAXF];   // line-search trial point
+  double acc[LR_MAXF];     // FedAvg accumulator
+  double g[LR_MAXF];       // gradient
+  double L[LR_MAXF * LR_MAXF];  // the Hessian's lower triangle, factorised in place (row-major)
+  double hv[LR_NMAX];      // s (1 - s) of the staged rows, s = sigma(-y z)
+  double sv[LR_NMAX];      // -y s
+  float xs[LR_NMAX * LR_MAXF];  // staged rows [i][k], k < F
+  float ys[LR_NMAX];       // +-1
+  int rid[LR_NMAX];
   double val_hist[64];
-  int done;
 };
 
-__device__ double block_sum(double v, double* red) {
-  const int tid = threadIdx.x;
-  red[tid] = v;
-  __syncthreads();
-  for (int off = LR_THREADS / 2; off >= 1; off >>= 1) {
-    if (tid < off) red[tid] += red[tid + off];
-    __syncthreads();
-  }
-  const double r = red[0];
-  __syncthreads();
-  return r;
+// Sum over the wave: an xor butterfly, so every lane ends with the same bits (each level adds the same two
+// partial sums on both partner lanes: a + b and b + a).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
 }
 
 // rows: global row ids of this fit are rowsel(i), i < n (row = rows[off + perm...]); X row-major [N][F]
@@ -62,151 +73,162 @@ struct RowSel {
   }
 };
 
-__device__ double objective(const double* w, const RowSel& rs, const float* X, const float* Y, int F, Shared& sh) {
-  double part = 0.0;
-  for (int i = threadIdx.x; i < rs.count; i += LR_THREADS) {
-    const int r = rs.row(i);
-    const float* xr = X + (int64_t)r * F;
-    double z = w[F];
-    for (int k = 0; k < F; ++k) z += w[k] * (double)xr[k];
-    const double yy = Y[r] > 0.5f ? 1.0 : -1.0;
-    const double t = -yy * z;
-    part += t > 0 ? t + log1p(exp(-t)) : log1p(exp(t));
+// rows [c0, c0 + cn) of the fit into LDS: features as fp32 (the data's own precision), labels as +-1
+__device__ void stage_rows(const RowSel& rs, int c0, int cn, const float* X, const float* Y, int F, Shared& sh) {
+  const int lane = threadIdx.x;
+  for (int i = lane; i < cn; i += LR_THREADS) {
+    const int r = rs.row(c0 + i);
+    sh.rid[i] = r;
+    sh.ys[i] = Y[r] > 0.5f ? 1.0f : -1.0f;
   }
-  double f = block_sum(part, sh.red);
-  double reg = 0.0;
-  for (int k = 0; k < F; ++k) reg += w[k] * w[k];
-  return f + 0.5 * reg;
+  __syncthreads();
+  for (int e = lane; e < cn * F; e += LR_THREADS) {
+    const int i = e / F, k = e % F;
+    sh.xs[i * LR_MAXF + k] = X[(int64_t)sh.rid[i] * F + k];
+  }
+  __syncthreads();
 }
 
-// Exact L2-logistic fit (damped Newton) into sh.w, warm-started from sh.w.
+__device__ __forceinline__ double row_z(const double* w, const float* xr, int F) {
+  double z = w[F];
+  for (int k = 0; k < F; ++k) z += w[k] * (double)xr[k];
+  return z;
+}
+
+// sum_i log(1 + exp(-y_i z_i)) + 0.5 ||coef||^2 over the fit's rows (staged already when resident)
+__device__ double objective(const double* w, const RowSel& rs, bool resident, const float* X, const float* Y, int F,
+                            Shared& sh) {
+  const int lane = threadIdx.x;
+  double part = 0.0;
+  for (int c0 = 0; c0 < rs.count; c0 += LR_NMAX) {
+    const int cn = min(LR_NMAX, rs.count - c0);
+    if (!resident) stage_rows(rs, c0, cn, X, Y, F, sh);
+    for (int i = lane; i < cn; i += LR_THREADS) {
+      const double t = -(double)sh.ys[i] * row_z(w, sh.xs + i * LR_MAXF, F);
+      part += t > 0 ? t + log1p(exp(-t)) : log1p(exp(t));
+    }
+  }
+  const double reg = (lane < F) ? w[lane] * w[lane] : 0.0;
+  return wave_sum(part) + 0.5 * wave_sum(reg);
+}
+
+// Exact L2-logistic fit (damped Newton with Armijo backtracking) into sh.w, warm-started from sh.w.
 __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int F, Shared& sh) {
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int D = F + 1;
+  const int NE = D * (D + 1) / 2 + D;  // Hessian entries (k <= l) then the gradient
+  const bool resident = rs.count <= LR_NMAX;
+  if (resident) stage_rows(rs, 0, rs.count, X, Y, F, sh);
+  double f0 = objective(sh.w, rs, resident, X, Y, F, sh);
   for (int it = 0; it < 100; ++it) {
-    // gradient and Hessian: rows staged in chunks (sigma and row id in LDS); thread t owns entries
-    // e = t, t+256, ... of [upper-triangular Hessian | gradient]
-    double accum[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int c0 = 0; c0 < rs.count; c0 += LR_CHUNK) {
-      const int cn = min(LR_CHUNK, rs.count - c0);
-      for (int i = tid; i < cn; i += LR_THREADS) {
-        const int r = rs.row(c0 + i);
-        const float* xr = X + (int64_t)r * F;
-        double z = sh.w[F];
-        for (int q = 0; q < F; ++q) z += sh.w[q] * (double)xr[q];
-        const double yy = Y[r] > 0.5f ? 1.0 : -1.0;
-        sh.sg[i] = 1.0 / (1.0 + exp(yy * z));
-        sh.rid[i] = r;
+    // gradient and Hessian: per staged row s and s (1 - s), then lane-owned entries summed over the rows in order
+    double acc[LR_EPL];
+#pragma unroll
+    for (int u = 0; u < LR_EPL; ++u) acc[u] = 0.0;
+    for (int c0 = 0; c0 < rs.count; c0 += LR_NMAX) {
+      const int cn = min(LR_NMAX, rs.count - c0);
+      if (!resident) stage_rows(rs, c0, cn, X, Y, F, sh);
+      for (int i = lane; i < cn; i += LR_THREADS) {
+        const double yy = (double)sh.ys[i];
+        const double sg = 1.0 / (1.0 + exp(yy * row_z(sh.w, sh.xs + i * LR_MAXF, F)));
+        sh.sv[i] = -yy * sg;
+        sh.hv[i] = sg * (1.0 - sg);
       }
       __syncthreads();
-      for (int u = 0, e = tid; e < D * D + D; e += LR_THREADS, ++u) {
-        const bool isg = e >= D * D;
-        const int k = isg ? e - D * D : e / D;
-        const int l = isg ? 0 : e % D;
-        if (!isg && l < k) continue;  // upper triangle only
+#pragma unroll
+      for (int u = 0; u < LR_EPL; ++u) {
+        const int e = lane + LR_THREADS * u;
+        if (e >= NE) break;
         double s = 0.0;
-        for (int i = 0; i < cn; ++i) {
-          const int r = sh.rid[i];
-          const float* xr = X + (int64_t)r * F;
-          const double sg = sh.sg[i];
-          const double xk = k < F ? (double)xr[k] : 1.0;
-          if (isg) {
-            const double yy = Y[r] > 0.5f ? 1.0 : -1.0;
-            s += -yy * sg * xk;
-          } else {
-            const double xl = l < F ? (double)xr[l] : 1.0;
-            s += sg * (1.0 - sg) * xk * xl;
+        if (e >= NE - D) {  // gradient entry k
+          const int k = e - (NE - D);
+          for (int i = 0; i < cn; ++i) s += sh.sv[i] * (k < F ? (double)sh.xs[i * LR_MAXF + k] : 1.0);
+        } else {  // Hessian entry (k, l), k <= l: the e-th of the row-major upper triangle
+          int k = 0, rem = e;
+          while (rem >= D - k) { rem -= D - k; ++k; }
+          const int l = k + rem;
+          for (int i = 0; i < cn; ++i) {
+            const double xk = k < F ? (double)sh.xs[i * LR_MAXF + k] : 1.0;
+            const double xl = l < F ? (double)sh.xs[i * LR_MAXF + l] : 1.0;
+            s += sh.hv[i] * xk * xl;
           }
         }
-        accum[u] += s;
+        acc[u] += s;
       }
       __syncthreads();
     }
-    for (int u = 0, e = tid; e < D * D + D; e += LR_THREADS, ++u) {
-      const bool isg = e >= D * D;
-      const int k = isg ? e - D * D : e / D;
-      const int l = isg ? 0 : e % D;
-      if (!isg && l < k) continue;
-      if (isg) {
-        sh.g[k] = accum[u] + (k < F ? sh.w[k] : 0.0);
+#pragma unroll
+    for (int u = 0; u < LR_EPL; ++u) {
+      const int e = lane + LR_THREADS * u;
+      if (e >= NE) break;
+      if (e >= NE - D) {
+        const int k = e - (NE - D);
+        sh.g[k] = acc[u] + (k < F ? sh.w[k] : 0.0);
       } else {
-        const double v = accum[u] + ((k == l && k < F) ? 1.0 : 0.0);
-        sh.H[k * D + l] = v;
-        sh.H[l * D + k] = v;
+        int k = 0, rem = e;
+        while (rem >= D - k) { rem -= D - k; ++k; }
+        const int l = k + rem;
+        sh.L[l * LR_MAXF + k] = acc[u] + ((k == l && k < F) ? 1.0 : 0.0);  // lower triangle, row l
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      double gmax = 0.0;
-      for (int k = 0; k < D; ++k) gmax = fmax(gmax, fabs(sh.g[k]));
-      sh.done = gmax < 1e-10 ? 1 : 0;
-    }
-    __syncthreads();
-    if (sh.done) break;
-    // Cholesky solve H d = g (single lane: D <= 64, negligible)
-    if (tid == 0) {
-      double* A = sh.H;
-      for (int j = 0; j < D; ++j) {
-        double s = A[j * D + j];
-        for (int q = 0; q < j; ++q) s -= A[j * D + q] * A[j * D + q];
-        const double Ljj = sqrt(s);
-        A[j * D + j] = Ljj;
-        for (int i = j + 1; i < D; ++i) {
-          double t = A[i * D + j];
-          for (int q = 0; q < j; ++q) t -= A[i * D + q] * A[j * D + q];
-          A[i * D + j] = t / Ljj;
-        }
+    const double gk = lane < D ? sh.g[lane] : 0.0;
+    if (wave_max(fabs(gk)) < 1e-10) break;
+    // Cholesky H = L L^T in place, left-looking: column j, lanes = rows i >= j
+    for (int j = 0; j < D; ++j) {
+      double sj = 0.0;
+      if (lane >= j && lane < D) {
+        sj = sh.L[lane * LR_MAXF + j];
+        for (int q = 0; q < j; ++q) sj -= sh.L[lane * LR_MAXF + q] * sh.L[j * LR_MAXF + q];
       }
-      for (int i = 0; i < D; ++i) {  // forward
-        double t = sh.g[i];
-        for (int q = 0; q < i; ++q) t -= A[i * D + q] * sh.d[q];
-        sh.d[i] = t / A[i * D + i];
-      }
-      for (int i = D - 1; i >= 0; --i) {  // backward
-        double t = sh.d[i];
-        for (int q = i + 1; q < D; ++q) t -= A[q * D + i] * sh.d[q];
-        sh.d[i] = t / A[i * D + i];
-      }
-    }
-    __syncthreads();
-    // backtracking line search on the objective
-    const double f0 = objective(sh.w, rs, X, Y, F, sh);
-    double gd = 0.0;
-    for (int k = 0; k < D; ++k) gd += sh.g[k] * sh.d[k];
-    double t = 1.0;
-    for (int ls = 0; ls < 40; ++ls) {
-      if (tid < D) sh.theta[tid] = sh.w[tid] - t * sh.d[tid];  // theta used as scratch trial point
+      const double ljj = sqrt(__shfl(sj, j));
+      if (lane == j) sh.L[j * LR_MAXF + j] = ljj;
+      else if (lane > j && lane < D) sh.L[lane * LR_MAXF + j] = sj / ljj;
       __syncthreads();
-      const double f1 = objective(sh.theta, rs, X, Y, F, sh);
+    }
+    // L y = g (forward), L^T d = y (backward): lane k holds entry k; one row broadcast per step
+    double b = gk;
+    for (int q = 0; q < D; ++q) {
+      const double yq = __shfl(b, q) / sh.L[q * LR_MAXF + q];
+      if (lane == q) b = yq;
+      else if (lane > q && lane < D) b -= sh.L[lane * LR_MAXF + q] * yq;
+    }
+    for (int q = D - 1; q >= 0; --q) {
+      const double dq = __shfl(b, q) / sh.L[q * LR_MAXF + q];
+      if (lane == q) b = dq;
+      else if (lane < q) b -= sh.L[q * LR_MAXF + lane] * dq;
+    }
+    const double dk = lane < D ? b : 0.0;
+    const double gd = wave_sum(gk * dk);
+    // backtracking line search on the objective; the accepted value is the next iteration's f0
+    double t = 1.0, f1 = f0;
+    for (int ls = 0; ls < 40; ++ls) {
+      if (lane < D) sh.trial[lane] = sh.w[lane] - t * dk;
+      __syncthreads();
+      f1 = objective(sh.trial, rs, resident, X, Y, F, sh);
       if (f1 <= f0 - 1e-4 * t * gd) break;
       t *= 0.5;
-      __syncthreads();
     }
-    if (tid < D) sh.w[tid] = sh.theta[tid];
+    if (lane < D) sh.w[lane] = sh.trial[lane];
+    f0 = f1;
     __syncthreads();
   }
 }
 
-__device__ int count_correct(const double* w, const float* X, const float* Y, int n, int F, double* red) {
+__device__ int count_correct(const double* w, const float* X, const float* Y, int n, int F) {
   double c = 0.0;
-  for (int i = threadIdx.x; i < n; i += LR_THREADS) {
-    double z = w[F];
-    for (int k = 0; k < F; ++k) z += w[k] * (double)X[(int64_t)i * F + k];
-    c += ((z > 0.0) == (Y[i] > 0.5f)) ? 1.0 : 0.0;
-  }
-  return (int)(block_sum(c, red) + 0.5);
+  for (int i = threadIdx.x; i < n; i += LR_THREADS)
+    c += ((row_z(w, X + (int64_t)i * F, F) > 0.0) == (Y[i] > 0.5f)) ? 1.0 : 0.0;
+  return (int)(wave_sum(c) + 0.5);
 }
 
-__device__ int count_correct_rows(const double* w, const RowSel& rs, const float* X, const float* Y, int F,
-                                  double* red) {
+__device__ int count_correct_rows(const double* w, const RowSel& rs, const float* X, const float* Y, int F) {
   double c = 0.0;
   for (int i = threadIdx.x; i < rs.count; i += LR_THREADS) {
     const int r = rs.row(i);
-    double z = w[F];
-    for (int k = 0; k < F; ++k) z += w[k] * (double)X[(int64_t)r * F + k];
-    c += ((z > 0.0) == (Y[r] > 0.5f)) ? 1.0 : 0.0;
+    c += ((row_z(w, X + (int64_t)r * F, F) > 0.0) == (Y[r] > 0.5f)) ? 1.0 : 0.0;
   }
-  return (int)(block_sum(c, red) + 0.5);
+  return (int)(wave_sum(c) + 0.5);
 }
 
 // Titanic.LogisticRegression.evaluate (mplc/dataset.py:343-351): [log_loss(y, predict(x)), accuracy] on hard
@@ -249,8 +271,8 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     if (tid < D) theta_out[(int64_t)c * D + tid] = sh.w[tid];
     __syncthreads();
     if (hist) {  // SinglePartnerLearning logs its fit at [0, 0]
-      const int ct = count_correct_rows(sh.w, rs, X, Y, F, sh.red);
-      const int cv = count_correct(sh.w, Xv, Yv, n_val, F, sh.red);
+      const int ct = count_correct_rows(sh.w, rs, X, Y, F);
+      const int cv = count_correct(sh.w, Xv, Yv, n_val, F);
       if (tid == 0) {
         double* h = hist + (int64_t)c * hist_stride + 2;
         lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
@@ -264,7 +286,7 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
       if (early_stopping && epochs > 10 && e < 64) {
         double vl = 0.0;
         if (have) {  // log_loss(y, predict(x)) on hard 0/1 predictions, sklearn eps 1e-15
-          const int cv = count_correct(sh.theta, Xv, Yv, n_val, F, sh.red);
+          const int cv = count_correct(sh.theta, Xv, Yv, n_val, F);
           const double eps = 1e-15;
           vl = (double)(n_val - cv) * (-log(eps)) / (double)n_val + (double)cv * (-log(1.0 - eps)) / (double)n_val;
         }
@@ -274,7 +296,7 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
       for (int m = 0; m < M; ++m) {
         double* hrow = hist ? hist + (int64_t)c * hist_stride + (int64_t)(e * M + m) * (2 + 4 * LR_MAXP) : nullptr;
         if (hrow) {  // the round-start collective model on val (eval_and_log_model_val_perf); unfitted: [0, 0]
-          const int cv = have ? count_correct(sh.theta, Xv, Yv, n_val, F, sh.red) : 0;
+          const int cv = have ? count_correct(sh.theta, Xv, Yv, n_val, F) : 0;
           if (tid == 0) {
             if (have) lr_metrics(cv, n_val, hrow[0], hrow[1], EPS_GLOBAL);
             else hrow[0] = hrow[1] = 0.0;
@@ -291,8 +313,8 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
           __syncthreads();
           newton_fit(rs, X, Y, F, sh);
           if (hrow) {  // the partner's fit history: [loss, accuracy] on its minibatch, then on val
-            const int ct = count_correct_rows(sh.w, rs, X, Y, F, sh.red);
-            const int cv = count_correct(sh.w, Xv, Yv, n_val, F, sh.red);
+            const int ct = count_correct_rows(sh.w, rs, X, Y, F);
+            const int cv = count_correct(sh.w, Xv, Yv, n_val, F);
             if (tid == 0) {
               double* h = hrow + 2 + 4 * pi;
               lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
@@ -319,7 +341,7 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     if (tid < D) sh.w[tid] = sh.theta[tid];
     __syncthreads();
   }
-  const int cc = count_correct(sh.w, Xt, Yt, n_test, F, sh.red);
+  const int cc = count_correct(sh.w, Xt, Yt, n_test, F);
   if (tid == 0) {
     correct[c] = cc;
     epochs_done[c] = done_epochs;
@@ -340,8 +362,8 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
     return MPLC_E_ARG;
   if (hist && (!x_val || !y_val || n_val < 1 || hist_stride < (int64_t)epochs * minibatch_count * (2 + 4 * LR_MAXP)))
     return MPLC_E_ARG;
-  // (D*D + D) Hessian+gradient entries must fit 4 per thread: D = n_features + 1 <= 31
-  if (n_features < 1 || n_features + 1 > 31 || n_coalitions < 1 || minibatch_count < 1 || epochs < 1 ||
+  // D = n_features + 1 unknowns <= LR_MAXF (the factor, the per-lane Hessian entries)
+  if (n_features < 1 || n_features + 1 > LR_MAXF || n_coalitions < 1 || minibatch_count < 1 || epochs < 1 ||
       n_test < 1)
     return MPLC_E_ARG;
   if (early_stopping && (!x_val || !y_val || n_val < 1)) return MPLC_E_ARG;
