@@ -11,39 +11,45 @@
 // One workgroup = one coalition; every fit is solved EXACTLY (damped Newton in fp64, gradient < 1e-10),
 // the optimum of the strictly convex problem sklearn approximates to tol 1e-4.
 // Work is tiny (28 unknowns, tens of rows): latency-bound; the point is doing all coalitions in ONE launch and
-// keeping each fit's dependent chain short.  Round 5: one wave per coalition (reductions in registers, no block
-// barriers), the fit's rows staged in LDS once per fit (the Newton iterations read them from LDS instead of
-// re-gathering them through the keyed permutation from global memory), the Hessian's entries spread over the
-// lanes, the Cholesky factorisation and the two triangular solves parallel over the rows (a single lane did them
-// serially: 28^3/6 dependent LDS round trips per iteration), and the line search's accepted objective reused as
-// the next iteration's start value.  The 1023-coalition sweep (config #2): 242 ms -> 40.3 ms
-// (profiles/r05_titanic_kernel_stats{,_onewave}.csv).
+// keeping each fit's dependent chain short.  Round 5: one wave per coalition.  The fit's rows are staged in LDS
+// once per fit as fp64 with the intercept's column of ones (lanes over rows, each row's loads issued together); the
+// Hessian X^T diag(h) X and the gradient come from v_mfma_f64_16x16x4 (2 x 2 tiles of 16, the gradient riding in
+// the padding column 31); lane i factorises row i of H in registers (right-looking Cholesky, multipliers broadcast
+// with v_readlane, the padding rows set to the identity so no loop needs a data-dependent guard); the solves run on
+// the lanes; wave sums are xor butterflies (the same bits on every lane, so every branch is uniform); the line
+// search's accepted objective is the next iteration's start value.  The 1023-coalition sweep (config #2):
+// 242 ms (one 256-thread workgroup, serial single-thread factorisation) -> 14.7 ms
+// (profiles/r05_titanic_kernel_stats{,_mfma}.csv; per-phase times: scripts/lr_phases.py, profiles/r05_lr_phases.json).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "keyed.h"
 #include "mplc_hip.h"
+
+// Phase-timing hooks (scripts/lr_phases.py builds a timing copy of this file that defines them); no-ops here.
+#ifndef LR_PHASE
+#define LR_PHASE(i) ((void)0)
+#endif
 
 namespace {
 
 constexpr int LR_THREADS = 64;   // one wave per coalition
 constexpr int LR_MAXF = 32;      // D = n_features + 1 unknowns (coef | intercept) supported
 constexpr int LR_MAXP = 64;      // partners per coalition
-constexpr int LR_NMAX = 128;     // rows staged in LDS at a time (a whole Titanic fit: <= 71 rows)
-constexpr int LR_NE = LR_MAXF * (LR_MAXF + 1) / 2 + LR_MAXF;  // Hessian upper triangle + gradient entries
-constexpr int LR_EPL = (LR_NE + LR_THREADS - 1) / LR_THREADS;  // entries per lane
+constexpr int LR_NMAX = 96;      // rows staged in LDS at a time (a whole Titanic fit: <= 71 rows)
+constexpr int LR_XS = LR_MAXF + 2;  // staged row stride in doubles: 16-byte aligned rows, 4-way banked per-lane reads
+constexpr int LR_LS = LR_MAXF + 1;  // row stride of the Hessian / factor in LDS: lane li's row reads 2-way banked
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 struct Shared {
   double theta[LR_MAXF];
-  double w[LR_MAXF];       // current Newton iterate
-  double trial[LR_MAXF];   // line-search trial point
+  double w[LR_MAXF];       // current Newton iterate (entries >= D stay 0)
+  double trial[LR_MAXF];   // line-search trial point (entries >= D stay 0)
   double acc[LR_MAXF];     // FedAvg accumulator
-  double g[LR_MAXF];       // gradient
-  double L[LR_MAXF * LR_MAXF];  // the Hessian's lower triangle, factorised in place (row-major)
+  double L[LR_MAXF * LR_LS];  // the Hessian's tiles, then the Cholesky factor (row-major, stride LR_LS)
   double hv[LR_NMAX];      // s (1 - s) of the staged rows, s = sigma(-y z)
   double sv[LR_NMAX];      // -y s
-  float xs[LR_NMAX * LR_MAXF];  // staged rows [i][k], k < F
-  float ys[LR_NMAX];       // +-1
-  int rid[LR_NMAX];
+  double xs[LR_NMAX * LR_XS];  // staged rows [i][k]: features k < F, 1 at k = F (the intercept's column), 0 after
+  double ys[LR_NMAX];      // +-1
   double val_hist[64];
 };
 
@@ -61,6 +67,13 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+// lane l's value of v, for every lane (v_readlane into scalar registers; l uniform)
+__device__ __forceinline__ double readlane(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 // rows: global row ids of this fit are rowsel(i), i < n (row = rows[off + perm...]); X row-major [N][F]
 struct RowSel {
   const int32_t* rows;
@@ -73,25 +86,30 @@ struct RowSel {
   }
 };
 
-// rows [c0, c0 + cn) of the fit into LDS: features as fp32 (the data's own precision), labels as +-1
+// rows [c0, c0 + cn) of the fit into LDS as fp64 (exact widening of the fp32 data), the intercept's column of ones
+// and zero padding appended, labels as +-1
 __device__ void stage_rows(const RowSel& rs, int c0, int cn, const float* X, const float* Y, int F, Shared& sh) {
-  const int lane = threadIdx.x;
-  for (int i = lane; i < cn; i += LR_THREADS) {
+  // lanes over rows: each lane gathers its row's F features with independent loads (one memory latency per row,
+  // not one per feature)
+  for (int i = threadIdx.x; i < cn; i += LR_THREADS) {
     const int r = rs.row(c0 + i);
-    sh.rid[i] = r;
-    sh.ys[i] = Y[r] > 0.5f ? 1.0f : -1.0f;
-  }
-  __syncthreads();
-  for (int e = lane; e < cn * F; e += LR_THREADS) {
-    const int i = e / F, k = e % F;
-    sh.xs[i * LR_MAXF + k] = X[(int64_t)sh.rid[i] * F + k];
+    sh.ys[i] = Y[r] > 0.5f ? 1.0 : -1.0;
+    const float* xr = X + (int64_t)r * F;
+    double* dst = sh.xs + i * LR_XS;
+    float v[LR_MAXF];
+#pragma unroll
+    for (int k = 0; k < LR_MAXF; ++k) v[k] = xr[min(k, F - 1)];  // unconditional: the loads issue back to back
+#pragma unroll
+    for (int k = 0; k < LR_MAXF; ++k) dst[k] = k < F ? (double)v[k] : (k == F ? 1.0 : 0.0);
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ double row_z(const double* w, const float* xr, int F) {
-  double z = w[F];
-  for (int k = 0; k < F; ++k) z += w[k] * (double)xr[k];
+// w . [x | 1] over a staged row (w's entries >= D are 0, as are the row's)
+__device__ __forceinline__ double row_z(const double* w, const double* xr) {
+  double z = 0.0;
+#pragma unroll
+  for (int k = 0; k < LR_MAXF; ++k) z += w[k] * xr[k];
   return z;
 }
 
@@ -104,102 +122,123 @@ __device__ double objective(const double* w, const RowSel& rs, bool resident, co
     const int cn = min(LR_NMAX, rs.count - c0);
     if (!resident) stage_rows(rs, c0, cn, X, Y, F, sh);
     for (int i = lane; i < cn; i += LR_THREADS) {
-      const double t = -(double)sh.ys[i] * row_z(w, sh.xs + i * LR_MAXF, F);
+      const double t = -sh.ys[i] * row_z(w, sh.xs + i * LR_XS);
       part += t > 0 ? t + log1p(exp(-t)) : log1p(exp(t));
     }
+    if (!resident) __syncthreads();
   }
   const double reg = (lane < F) ? w[lane] * w[lane] : 0.0;
   return wave_sum(part) + 0.5 * wave_sum(reg);
 }
 
 // Exact L2-logistic fit (damped Newton with Armijo backtracking) into sh.w, warm-started from sh.w.
+// Lane i (< D) owns row i of the Hessian in registers (h[k], k < LR_MAXF: fully unrolled, so every index is a
+// compile-time constant), factorises it in place (right-looking Cholesky, column j's multipliers broadcast with
+// v_readlane) and holds entry i of the gradient and of the Newton step.
 __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int F, Shared& sh) {
   const int lane = threadIdx.x;
+  const int li = lane & (LR_MAXF - 1);  // the Hessian row this lane factorises (lanes >= 32 mirror lanes < 32)
   const int D = F + 1;
-  const int NE = D * (D + 1) / 2 + D;  // Hessian entries (k <= l) then the gradient
   const bool resident = rs.count <= LR_NMAX;
   if (resident) stage_rows(rs, 0, rs.count, X, Y, F, sh);
+  LR_PHASE(9);
   double f0 = objective(sh.w, rs, resident, X, Y, F, sh);
+  LR_PHASE(1);
+  const int kk = lane >> 4, idx = lane & 15;  // the f64 MFMA's operand lane map: A[idx][kk], B[kk][idx]
   for (int it = 0; it < 100; ++it) {
-    // gradient and Hessian: per staged row s and s (1 - s), then lane-owned entries summed over the rows in order
-    double acc[LR_EPL];
-#pragma unroll
-    for (int u = 0; u < LR_EPL; ++u) acc[u] = 0.0;
+    // H = sum_r x_r (h_r x_r)^T on the matrix cores: 32 x 32 as 2 x 2 tiles of v_mfma_f64_16x16x4, four rows per
+    // step.  B's column 31 (the padding column: D <= 31) carries sv_r instead, so that column of the product is
+    // the gradient's data term sum_r sv_r x_r.
+    f64x4 t00 = {0.0, 0.0, 0.0, 0.0}, t01 = t00, t10 = t00, t11 = t00;
     for (int c0 = 0; c0 < rs.count; c0 += LR_NMAX) {
       const int cn = min(LR_NMAX, rs.count - c0);
+      const int cn4 = (cn + 3) & ~3;
       if (!resident) stage_rows(rs, c0, cn, X, Y, F, sh);
-      for (int i = lane; i < cn; i += LR_THREADS) {
-        const double yy = (double)sh.ys[i];
-        const double sg = 1.0 / (1.0 + exp(yy * row_z(sh.w, sh.xs + i * LR_MAXF, F)));
-        sh.sv[i] = -yy * sg;
-        sh.hv[i] = sg * (1.0 - sg);
+      for (int i = lane; i < cn4; i += LR_THREADS) {  // per row: s = sigma(-y z), s (1 - s); 0 on the padding
+        double sv = 0.0, hv = 0.0;
+        if (i < cn) {
+          const double yy = sh.ys[i];
+          const double sg = 1.0 / (1.0 + exp(yy * row_z(sh.w, sh.xs + i * LR_XS)));
+          sv = -yy * sg;
+          hv = sg * (1.0 - sg);
+        }
+        sh.sv[i] = sv;
+        sh.hv[i] = hv;
       }
       __syncthreads();
-#pragma unroll
-      for (int u = 0; u < LR_EPL; ++u) {
-        const int e = lane + LR_THREADS * u;
-        if (e >= NE) break;
-        double s = 0.0;
-        if (e >= NE - D) {  // gradient entry k
-          const int k = e - (NE - D);
-          for (int i = 0; i < cn; ++i) s += sh.sv[i] * (k < F ? (double)sh.xs[i * LR_MAXF + k] : 1.0);
-        } else {  // Hessian entry (k, l), k <= l: the e-th of the row-major upper triangle
-          int k = 0, rem = e;
-          while (rem >= D - k) { rem -= D - k; ++k; }
-          const int l = k + rem;
-          for (int i = 0; i < cn; ++i) {
-            const double xk = k < F ? (double)sh.xs[i * LR_MAXF + k] : 1.0;
-            const double xl = l < F ? (double)sh.xs[i * LR_MAXF + l] : 1.0;
-            s += sh.hv[i] * xk * xl;
-          }
-        }
-        acc[u] += s;
+      for (int r0 = 0; r0 < cn; r0 += 4) {
+        const int r = r0 + kk;
+        const bool ok = r < cn;
+        const double a0 = ok ? sh.xs[r * LR_XS + idx] : 0.0;
+        const double a1 = ok ? sh.xs[r * LR_XS + 16 + idx] : 0.0;
+        const double hr = sh.hv[r];
+        const double b0 = hr * a0;
+        const double b1 = idx == 15 ? sh.sv[r] : hr * a1;
+        t00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t00, 0, 0, 0);
+        t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, t01, 0, 0, 0);
+        t10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, t10, 0, 0, 0);
+        t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t11, 0, 0, 0);
       }
       __syncthreads();
     }
+    // tiles -> LDS (result v of a lane: row kk + 4 v, column idx) -> lane li takes row li
 #pragma unroll
-    for (int u = 0; u < LR_EPL; ++u) {
-      const int e = lane + LR_THREADS * u;
-      if (e >= NE) break;
-      if (e >= NE - D) {
-        const int k = e - (NE - D);
-        sh.g[k] = acc[u] + (k < F ? sh.w[k] : 0.0);
-      } else {
-        int k = 0, rem = e;
-        while (rem >= D - k) { rem -= D - k; ++k; }
-        const int l = k + rem;
-        sh.L[l * LR_MAXF + k] = acc[u] + ((k == l && k < F) ? 1.0 : 0.0);  // lower triangle, row l
-      }
+    for (int v = 0; v < 4; ++v) {
+      const int row = kk + 4 * v;
+      sh.L[row * LR_LS + idx] = t00[v];
+      sh.L[row * LR_LS + 16 + idx] = t01[v];
+      sh.L[(16 + row) * LR_LS + idx] = t10[v];
+      sh.L[(16 + row) * LR_LS + 16 + idx] = t11[v];
     }
     __syncthreads();
-    const double gk = lane < D ? sh.g[lane] : 0.0;
+    double h[LR_MAXF];
+#pragma unroll
+    for (int k = 0; k < LR_MAXF - 1; ++k) h[k] = sh.L[li * LR_LS + k];
+    h[LR_MAXF - 1] = 0.0;
+    const double gdata = sh.L[li * LR_LS + LR_MAXF - 1];
+    __syncthreads();
+    const double gk = li < D ? gdata + (li < F ? sh.w[li] : 0.0) : 0.0;
+    LR_PHASE(2);
     if (wave_max(fabs(gk)) < 1e-10) break;
-    // Cholesky H = L L^T in place, left-looking: column j, lanes = rows i >= j
-    for (int j = 0; j < D; ++j) {
-      double sj = 0.0;
-      if (lane >= j && lane < D) {
-        sj = sh.L[lane * LR_MAXF + j];
-        for (int q = 0; q < j; ++q) sj -= sh.L[lane * LR_MAXF + q] * sh.L[j * LR_MAXF + q];
-      }
-      const double ljj = sqrt(__shfl(sj, j));
-      if (lane == j) sh.L[j * LR_MAXF + j] = ljj;
-      else if (lane > j && lane < D) sh.L[lane * LR_MAXF + j] = sj / ljj;
-      __syncthreads();
+    LR_PHASE(3);
+    // the L2 term on the coefficients, and the identity on the padding rows li >= D: the factor of [H 0; 0 I] is
+    // [L 0; 0 I] exactly (every update of a padding entry subtracts an exact 0), so every loop below runs over all
+    // LR_MAXF columns with no data-dependent guard and no exec-mask branches
+#pragma unroll
+    for (int k = 0; k < LR_MAXF; ++k) h[k] += (k == li && (li < F || li >= D)) ? 1.0 : 0.0;
+    // Cholesky H = L L^T, right-looking: column j's multipliers l_ij = h[j] / l_jj on the lanes, then the trailing
+    // update h[k] -= l_ij l_kj (on every lane: the entries above the diagonal are never read).  The diagonal keeps
+    // 1 / l_jj, the only form the solves use.
+#pragma unroll
+    for (int j = 0; j < LR_MAXF; ++j) {
+      const double rinv = 1.0 / sqrt(readlane(h[j], j));
+      h[j] = (li == j) ? rinv : h[j] * rinv;
+#pragma unroll
+      for (int k = j + 1; k < LR_MAXF; ++k) h[k] -= h[j] * readlane(h[j], k);
     }
-    // L y = g (forward), L^T d = y (backward): lane k holds entry k; one row broadcast per step
+    LR_PHASE(4);
+    // L y = g (forward, L's column q in registers), L^T d = y (backward, L's row q from LDS)
+    if (lane < LR_MAXF) {
+#pragma unroll
+      for (int k = 0; k < LR_MAXF; ++k) sh.L[lane * LR_LS + k] = h[k];
+    }
     double b = gk;
-    for (int q = 0; q < D; ++q) {
-      const double yq = __shfl(b, q) / sh.L[q * LR_MAXF + q];
-      if (lane == q) b = yq;
-      else if (lane > q && lane < D) b -= sh.L[lane * LR_MAXF + q] * yq;
+#pragma unroll
+    for (int q = 0; q < LR_MAXF; ++q) {
+      const double yq = readlane(b, q) * readlane(h[q], q);
+      const double nb = b - h[q] * yq;
+      b = li > q ? nb : (li == q ? yq : b);
     }
-    for (int q = D - 1; q >= 0; --q) {
-      const double dq = __shfl(b, q) / sh.L[q * LR_MAXF + q];
-      if (lane == q) b = dq;
-      else if (lane < q) b -= sh.L[q * LR_MAXF + lane] * dq;
+    __syncthreads();
+#pragma unroll
+    for (int q = LR_MAXF - 1; q >= 0; --q) {
+      const double dq = readlane(b, q) * sh.L[q * LR_LS + q];
+      const double nb = b - sh.L[q * LR_LS + li] * dq;
+      b = li < q ? nb : (li == q ? dq : b);
     }
-    const double dk = lane < D ? b : 0.0;
-    const double gd = wave_sum(gk * dk);
+    const double dk = li < D ? b : 0.0;
+    LR_PHASE(5);
+    const double gd = wave_sum(lane < 32 ? gk * dk : 0.0);
     // backtracking line search on the objective; the accepted value is the next iteration's f0
     double t = 1.0, f1 = f0;
     for (int ls = 0; ls < 40; ++ls) {
@@ -211,14 +250,21 @@ __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int
     }
     if (lane < D) sh.w[lane] = sh.trial[lane];
     f0 = f1;
+    LR_PHASE(6);
     __syncthreads();
   }
+}
+
+__device__ __forceinline__ double row_z_global(const double* w, const float* xr, int F) {
+  double z = w[F];
+  for (int k = 0; k < F; ++k) z += w[k] * (double)xr[k];
+  return z;
 }
 
 __device__ int count_correct(const double* w, const float* X, const float* Y, int n, int F) {
   double c = 0.0;
   for (int i = threadIdx.x; i < n; i += LR_THREADS)
-    c += ((row_z(w, X + (int64_t)i * F, F) > 0.0) == (Y[i] > 0.5f)) ? 1.0 : 0.0;
+    c += ((row_z_global(w, X + (int64_t)i * F, F) > 0.0) == (Y[i] > 0.5f)) ? 1.0 : 0.0;
   return (int)(wave_sum(c) + 0.5);
 }
 
@@ -226,7 +272,7 @@ __device__ int count_correct_rows(const double* w, const RowSel& rs, const float
   double c = 0.0;
   for (int i = threadIdx.x; i < rs.count; i += LR_THREADS) {
     const int r = rs.row(i);
-    c += ((row_z(w, X + (int64_t)r * F, F) > 0.0) == (Y[r] > 0.5f)) ? 1.0 : 0.0;
+    c += ((row_z_global(w, X + (int64_t)r * F, F) > 0.0) == (Y[r] > 0.5f)) ? 1.0 : 0.0;
   }
   return (int)(wave_sum(c) + 0.5);
 }
@@ -252,20 +298,18 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     int32_t* __restrict__ correct, int32_t* __restrict__ epochs_done, double* __restrict__ theta_out,
     double* __restrict__ hist, int64_t hist_stride) {
   __shared__ Shared sh;
+  LR_PHASE(-1);
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
   const int D = F + 1;
   const uint64_t mask = masks[c];
-  int parts[LR_MAXP];
-  int P = 0;
-  for (int p = 0; p < 64 && P < LR_MAXP; ++p)
-    if ((mask >> p) & 1ull) parts[P++] = p;
-  if (tid < D) { sh.theta[tid] = 0.0; sh.w[tid] = 0.0; }
+  const int P = __popcll(mask);  // partners in bit order (no per-lane array: it would live in scratch memory)
+  if (tid < LR_MAXF) { sh.theta[tid] = 0.0; sh.w[tid] = 0.0; sh.trial[tid] = 0.0; }
   __syncthreads();
   int done_epochs = epochs;
   if (P == 1) {
     // singleton: one fit on the partner's full data (E refits of the same rows reach the same optimum)
-    const int p = parts[0];
+    const int p = __builtin_ctzll(mask);
     RowSel rs{rows, rows_off[p], n_rows[p], 0, n_rows[p], 0ull, false};
     newton_fit(rs, X, Y, F, sh);
     if (tid < D) theta_out[(int64_t)c * D + tid] = sh.w[tid];
@@ -304,13 +348,15 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
         }
         if (tid < D) sh.acc[tid] = 0.0;
         __syncthreads();
-        for (int pi = 0; pi < P; ++pi) {
-          const int p = parts[pi];
+        uint64_t rem = mask;
+        for (int pi = 0; pi < P; ++pi, rem &= rem - 1) {
+          const int p = __builtin_ctzll(rem);
           const int* sp = splits + p * (M + 1);
           RowSel rs{rows, rows_off[p], n_rows[p], sp[m], sp[m + 1] - sp[m],
                     subkey(keys[(int64_t)c * LR_MAXP + pi], 0x10000u + (uint32_t)e, 0u), M > 1};
           if (tid < D) sh.w[tid] = have ? sh.theta[tid] : 0.0;  // warm start from the global model
           __syncthreads();
+          LR_PHASE(10);
           newton_fit(rs, X, Y, F, sh);
           if (hrow) {  // the partner's fit history: [loss, accuracy] on its minibatch, then on val
             const int ct = count_correct_rows(sh.w, rs, X, Y, F);
@@ -329,6 +375,7 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
           __syncthreads();
         }
         if (tid < D) sh.theta[tid] = sh.acc[tid] / agg_scale[c];
+        LR_PHASE(8);
         have = 1;
         __syncthreads();
       }
@@ -341,6 +388,7 @@ __global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
     if (tid < D) sh.w[tid] = sh.theta[tid];
     __syncthreads();
   }
+  LR_PHASE(7);
   const int cc = count_correct(sh.w, Xt, Yt, n_test, F);
   if (tid == 0) {
     correct[c] = cc;
@@ -362,8 +410,8 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
     return MPLC_E_ARG;
   if (hist && (!x_val || !y_val || n_val < 1 || hist_stride < (int64_t)epochs * minibatch_count * (2 + 4 * LR_MAXP)))
     return MPLC_E_ARG;
-  // D = n_features + 1 unknowns <= LR_MAXF (the factor, the per-lane Hessian entries)
-  if (n_features < 1 || n_features + 1 > LR_MAXF || n_coalitions < 1 || minibatch_count < 1 || epochs < 1 ||
+  // D = n_features + 1 unknowns <= LR_MAXF - 1 (the Hessian product's last column carries the gradient)
+  if (n_features < 1 || n_features + 2 > LR_MAXF || n_coalitions < 1 || minibatch_count < 1 || epochs < 1 ||
       n_test < 1)
     return MPLC_E_ARG;
   if (early_stopping && (!x_val || !y_val || n_val < 1)) return MPLC_E_ARG;

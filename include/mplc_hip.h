@@ -102,7 +102,7 @@ int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, const int32_t* 
  *  splits: M+1 minibatch boundaries per partner (partner p at p*(M+1)); masks[c]: coalition bitmask;
  *  keys[c*64 + i], agg_w[c*64 + i]: shuffle key and aggregation weight of the i-th partner (ascending id)
  *  of coalition c; agg_scale[c]: np.average's weight sum.  Outputs: correct[c] test hits,
- *  epochs_done[c], theta_out[c][n_features+1] = [coef | intercept].  n_features <= 31 (one wave per coalition: 64 threads).
+ *  epochs_done[c], theta_out[c][n_features+1] = [coef | intercept].  n_features <= 30.
  *  hist (NULL = off; needs x_val): the learning history (mplc/mpl_utils.py:11-27, logged by
  *  mplc/multi_partner_learning.py:130-156) of coalition c at hist + c * hist_stride, round (e, m) at
  *  offset (e*M + m) * (2 + 4*64): [collective val_loss, val_accuracy at the round start (0, 0 while
