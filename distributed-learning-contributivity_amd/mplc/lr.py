@@ -13,6 +13,58 @@ from .fedavg import aggregation_weights
 MAXP = 64
 
 
+def _mix64_np(z):
+    """cnn.mix64 on a uint64 array (numpy's uint64 products wrap mod 2^64, the & M64 of the scalar form)."""
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def coalition_tables(coalitions, partner_sizes, seed, aggregation):
+    """The launch's per-coalition tables, vectorised over coalitions: bit masks, each member's shuffle key
+    (cnn.shuffle_key), the np.average weights and scale of aggregation_weights.  Equal, element for element, to
+    the per-coalition loop (tests/test_lr.py); the loop cost about 35 ms per 1023-coalition sweep on the host."""
+    C = len(coalitions)
+    n = len(partner_sizes)
+    member = np.zeros((C, n), dtype=bool)
+    for ci, c in enumerate(coalitions):
+        if len(c) > MAXP or (len(c) and c[-1] >= n):
+            raise ValueError(f"invalid coalition {c}")
+        member[ci, list(c)] = True
+    bits = np.left_shift(np.uint64(1), np.arange(n, dtype=np.uint64))
+    masks = (member * bits).sum(axis=1, dtype=np.uint64)
+    counts = member.sum(axis=1)
+    # member i of a coalition = the i-th set bit: its partner id
+    order = np.argsort(~member, axis=1, kind="stable")[:, :min(n, MAXP)]
+    slot = np.arange(order.shape[1])[None, :] < counts[:, None]
+    with np.errstate(over="ignore"):
+        base = _mix64_np(np.full(C, _mix64_np(np.array([(seed + 0x5EED) & ((1 << 64) - 1)], dtype=np.uint64))[0],
+                                 dtype=np.uint64) ^ masks)
+        k = _mix64_np(base[:, None] ^ (order.astype(np.uint64) + np.uint64(1)))
+    keys = np.zeros((C, MAXP), dtype=np.uint64)
+    keys[:, :order.shape[1]] = np.where(slot, k, np.uint64(0))
+    w = np.zeros((C, MAXP), dtype=np.float64)
+    scale = np.ones(C, dtype=np.float64)
+    sizes = np.asarray(partner_sizes)
+    for P in np.unique(counts):  # one vectorised aggregation_weights per coalition size (same reductions)
+        if P < 2:
+            continue
+        sel = np.nonzero(counts == P)[0]
+        sz = sizes[order[sel, :P]]
+        if aggregation == "uniform":
+            ww = np.full((len(sel), P), 1 / P)
+        elif aggregation == "data-volume":
+            ww = sz / np.sum(sz, axis=1, keepdims=True)
+        else:
+            raise ValueError(f"aggregation approach '{aggregation}' is not a valid approach. ")
+        scl = ww.sum(axis=1)
+        if np.any(scl == 0.0):
+            raise ZeroDivisionError("Weights sum to zero, can't be normalized")
+        w[sel, :P] = ww
+        scale[sel] = scl
+    return masks, keys, w, scale
+
+
 class LogRegEngine:
     def __init__(self, *, x_train, y_train, x_val, y_val, x_test, y_test, partner_rows, epoch_count, minibatch_count,
                  aggregation="data-volume", is_early_stopping=True, seed=0, device=None, **_):
@@ -68,21 +120,7 @@ class LogRegEngine:
             raise ValueError("record_history takes exactly one coalition")
         E = self.epoch_count if epoch_count is None else int(epoch_count)
         es = self.is_early_stopping if is_early_stopping is None else bool(is_early_stopping)
-        masks = np.zeros(C, dtype=np.uint64)
-        keys = np.zeros((C, MAXP), dtype=np.uint64)
-        w = np.zeros((C, MAXP), dtype=np.float64)
-        scale = np.ones(C, dtype=np.float64)
-        for ci, c in enumerate(coalitions):
-            if len(c) > MAXP or c[-1] >= len(self.partner_sizes):
-                raise ValueError(f"invalid coalition {c}")
-            mask = sum(1 << p for p in c)
-            masks[ci] = mask
-            for i, p in enumerate(c):
-                keys[ci, i] = shuffle_key(self.seed, mask, p)
-            if len(c) > 1:
-                ww, scl = aggregation_weights([self.partner_sizes[p] for p in c], self.aggregation)
-                w[ci, :len(c)] = ww
-                scale[ci] = scl
+        masks, keys, w, scale = coalition_tables(coalitions, self.partner_sizes, self.seed, self.aggregation)
         dev = self.device
         t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
         masks_d = t(masks.view(np.int64))

@@ -166,3 +166,39 @@ def test_titanic_scenario_run_records_history_and_federated_sbs(golden):
         rel = (rel / hist["mpl_model"]["val_accuracy"].reshape(E * M)[:, None])[0:2]
         np.testing.assert_array_equal(const.contributivity_scores, np.nanmean(rel, axis=0))
     assert np.all(np.isinf(const.contributivity_scores))
+
+
+@pytest.mark.parametrize("n, seed, agg", [(10, 0, "data-volume"), (10, 7, "uniform"), (20, 3, "data-volume"),
+                                          (64, 11, "data-volume"), (13, 2 ** 63 + 5, "data-volume")])
+def test_launch_tables_equal_the_per_coalition_loop(n, seed, agg):
+    """mplc.lr.coalition_tables (vectorised) against the per-coalition loop it replaced: masks, every member's
+    shuffle key, the np.average weights and scale, bit for bit."""
+    from itertools import combinations
+
+    from mplc.cnn import shuffle_key
+    from mplc.fedavg import aggregation_weights
+    from mplc.lr import MAXP, coalition_tables
+    rng = np.random.default_rng(n + seed % 97)
+    sizes = [int(v) for v in rng.integers(1, 500, size=n)]
+    if n <= 10:
+        coals = [c for k in range(1, n + 1) for c in combinations(range(n), k)]
+    else:
+        coals = [tuple(sorted(rng.choice(n, size=int(rng.integers(1, n + 1)), replace=False).tolist()))
+                 for _ in range(300)]
+    C = len(coals)
+    masks, keys = np.zeros(C, dtype=np.uint64), np.zeros((C, MAXP), dtype=np.uint64)
+    w, scale = np.zeros((C, MAXP)), np.ones(C)
+    for ci, c in enumerate(coals):
+        mask = sum(1 << p for p in c)
+        masks[ci] = mask
+        for i, p in enumerate(c):
+            keys[ci, i] = shuffle_key(seed, mask, p)
+        if len(c) > 1:
+            ww, scl = aggregation_weights([sizes[p] for p in c], agg)
+            w[ci, :len(c)] = ww
+            scale[ci] = scl
+    got = coalition_tables(coals, sizes, seed, agg)
+    for a, b in zip((masks, keys, w, scale), got):
+        assert a.dtype == b.dtype and np.array_equal(a, b)
+    with pytest.raises(ValueError):
+        coalition_tables([(0, n)], sizes, seed, agg)
