@@ -642,8 +642,10 @@ def build_cifar_scenario(epochs, signal, partners=20):
 
 def cifar_kernel_table(timer, units):
     """Config #4's per-kernel table (as kernel_table for config #3): launches, in-stream ms, time share, and for
-    the convolutions (their algorithm's FLOPs: Winograd for conv2..conv4) and the W5 kernels (HBM bytes,
-    CifarModel.algorithmic_units) the achieved rate against the roofline."""
+    the convolutions (their algorithm's FLOPs: Winograd for conv2..conv4; conv1, under the ridge, its HBM bytes with
+    the FLOP rate beside) and the W5 kernels (HBM bytes, CifarModel.algorithmic_units) the achieved rate against the
+    roofline."""
+    from mplc.cifar import BYTES_PER_SAMPLE as CIFAR_BYTES_PER_SAMPLE
     from mplc.cifar import FLOP_PER_SAMPLE, KERNEL_IDS
     tot = sum(timer.total_ms(k) for k in KERNEL_IDS) or 1.0
     out = {}
@@ -651,7 +653,15 @@ def cifar_kernel_table(timer, units):
         ms, n = timer.total_ms(k), timer.launches(k)
         e = {"launches": n, "ms_total": round(ms, 1), "ms_avg": round(ms / max(1, n), 4), "time_share": round(ms / tot, 4)}
         if ms > 0 and units:
-            if k in FLOP_PER_SAMPLE:
+            if k in CIFAR_BYTES_PER_SAMPLE:  # under the ridge (conv1, K = 27): HBM-bound; the MFMA rate beside it
+                amount = units["samples"] * CIFAR_BYTES_PER_SAMPLE[k]
+                rate, peak, unit, bound = amount / (ms / 1000) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+                desc = (f"{k}'s compulsory HBM bytes ({CIFAR_BYTES_PER_SAMPLE[k]} per sample: "
+                        f"{FLOP_PER_SAMPLE[k] / CIFAR_BYTES_PER_SAMPLE[k]:.1f} flop/B, under the "
+                        f"{FP32_MFMA_PEAK_TFLOPS / HBM_PEAK_GBS * 1000:.1f} flop/B ridge)")
+                mf = units["samples"] * FLOP_PER_SAMPLE[k] / (ms / 1000) / 1e12
+                e["mfma_rate"] = {"achieved": round(mf, 2), "unit": "TFLOP/s", "frac": round(mf / FP32_MFMA_PEAK_TFLOPS, 4)}
+            elif k in FLOP_PER_SAMPLE:
                 amount = units["samples"] * FLOP_PER_SAMPLE[k]
                 rate, peak, unit, bound = amount / (ms / 1000) / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
                 desc = f"{k}'s fp32 multiply-adds ({FLOP_PER_SAMPLE[k]} per sample)"

@@ -18,6 +18,7 @@ STRIDE = 1251008
 NPARAM = 1250954
 WG_SAMPLES = 2
 A1, D2, A3, D4, H5 = 32768, 7200, 14400, 2304, 512
+IMG_FLOATS = 32 * 32 * 3
 DZ4, DZ3, DZ2, DZ1 = 2304, 14400, 7200, 32768  # dz4 / dz2: the pooled gradients (ABI 3)
 WT, WPART = 114688, 65664  # MPLC_CIFAR_WT: conv2..conv4 in Winograd form
 EVAL_FLOATS = A1 + D2 + A3 + D4 + H5  # per model per evaluated sample
@@ -41,6 +42,13 @@ DIRECT_FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 900 * 32
                           "conv2_dgrad": 900 * 32 * 288 * 2, "conv4_wgrad": 144 * 64 * 576 * 2,
                           "conv3_wgrad": 225 * 64 * 288 * 2, "conv2_wgrad": 900 * 32 * 288 * 2,
                           "conv1_wgrad": 1024 * 32 * 27 * 2}
+
+# conv1's algorithmic HBM bytes per sample: K = 27 (3 input channels) gives it 2 x 27 = 54 flops per output value,
+# 12.3 flops per byte of its compulsory traffic, under the fp32 MFMA / HBM ridge (157.3 / 8 = 19.7): its roofline is
+# HBM.  fwd: the image read (32 x 32 x 3 fp32) and a1 written (32 x 32 x 32 fp32); wgrad: the image and dz1 read
+# (dz1 = conv2's data gradient through relu', written by conv2_dgrad), the per-group dW1 partials (27 x 32 + 32
+# floats per MPLC_CIFAR_WG_SAMPLES samples) are not counted.
+BYTES_PER_SAMPLE = {"conv1_fwd": 4 * (IMG_FLOATS + A1), "conv1_wgrad": 4 * (IMG_FLOATS + DZ1)}
 
 
 class CifarTrainT(ctypes.Structure):

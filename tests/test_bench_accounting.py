@@ -83,3 +83,27 @@ def test_steps_of_batches_with_different_replica_counts():
     # batch b's step: coalition row 0 read once by its two first-step replicas
     per_sample_fwd = 9216 * 4 + 128 * 4
     assert ub["dense_fwd_bytes"] == 3 * W3 + W3 + 79 * per_sample_fwd  # three own rows + the shared one
+
+
+def test_cifar_table_puts_conv1_on_its_hbm_roof():
+    """conv1 (K = 27) sits under the fp32 MFMA / HBM ridge: its row is HBM-bound on its compulsory bytes, with the
+    MFMA rate beside it; the Winograd convolutions stay MFMA-bound."""
+    import bench
+    from mplc.cifar import BYTES_PER_SAMPLE, FLOP_PER_SAMPLE
+
+    class FakeTimer:
+        def total_ms(self, k):
+            return 2.0
+
+        def launches(self, k):
+            return 4
+
+    units = {"samples": 10000.0, "dense5_bwd_bytes": 1e10, "dense5_fwd_bytes": 2e9}
+    tab = bench.cifar_kernel_table(FakeTimer(), units)
+    c1 = tab["conv1_fwd"]
+    assert c1["bound"] == "hbm" and c1["unit"] == "GB/s"
+    assert c1["achieved"] == pytest.approx(10000 * BYTES_PER_SAMPLE["conv1_fwd"] / 0.002 / 1e9, rel=1e-6)
+    assert FLOP_PER_SAMPLE["conv1_fwd"] / BYTES_PER_SAMPLE["conv1_fwd"] < bench.FP32_MFMA_PEAK_TFLOPS / bench.HBM_PEAK_GBS * 1e3
+    assert c1["mfma_rate"]["achieved"] == pytest.approx(10000 * FLOP_PER_SAMPLE["conv1_fwd"] / 0.002 / 1e12, abs=0.01)
+    assert tab["conv1_wgrad"]["bound"] == "hbm" and tab["conv4_fwd"]["bound"] == "mfma"
+    assert tab["dense5_bwd"]["bound"] == "hbm"
