@@ -8,20 +8,23 @@
 //           early stop compares the round-0 val loss of epoch e with e - 10 (mplc/multi_partner_learning.py:
 //           177-193), where the never-fitted model of epoch 0 evaluates to [0, 0] (mplc/dataset.py:343-351)
 //   score   accuracy of predict() = [w.x + b > 0] on the test set
-// One workgroup = one coalition; every fit is solved EXACTLY (damped Newton in fp64, gradient < 1e-10),
-// the optimum of the strictly convex problem sklearn approximates to tol 1e-4.
-// Work is tiny (28 unknowns, tens of rows): latency-bound; the point is doing all coalitions in ONE launch and
-// keeping each fit's dependent chain short.  Round 5: one wave per coalition.  The fit's rows are staged in LDS
-// once per fit as fp64 with the intercept's column of ones (lanes over rows, each row's loads issued together); the
-// Hessian X^T diag(h) X and the gradient come from v_mfma_f64_16x16x4 (2 x 2 tiles of 16, the gradient riding in
-// the padding column 31); lane i factorises row i of H in registers (right-looking Cholesky, multipliers broadcast
-// with v_readlane, the padding rows set to the identity so no loop needs a data-dependent guard); the solves run on
-// the lanes; wave sums are xor butterflies (the same bits on every lane, so every branch is uniform); the line
-// search's accepted objective is the next iteration's start value.  The 1023-coalition sweep (config #2):
-// 242 ms (one 256-thread workgroup, serial single-thread factorisation) -> 14.7 ms
-// (profiles/r05_titanic_kernel_stats{,_mfma}.csv; per-phase times: scripts/lr_phases.py, profiles/r05_lr_phases.json).
+// Every fit is solved EXACTLY (damped Newton in fp64, gradient < 1e-10), the optimum of the strictly convex
+// problem sklearn approximates to tol 1e-4.  Work is tiny (28 unknowns, tens of rows): latency-bound; the point is
+// running all coalitions' fits together and keeping each fit's dependent chain short.  Round 5: each FedAvg round is one launch whose waves take
+// (coalition, partner) fits from a work queue, and one launch averages each coalition's fits (numpy's order, no
+// fused multiply-add).  A fit: its rows staged in LDS as fp64 with the intercept's column of ones; the Hessian
+// X^T diag(h) X and the gradient from v_mfma_f64_16x16x4 (2 x 2 tiles of 16, the gradient riding in the padding
+// column 31); lane i factorises row i of H in registers (right-looking Cholesky, multipliers broadcast with
+// v_readlane, the padding rows set to the identity so no loop needs a data-dependent guard); the solves on the
+// lanes; wave sums as xor butterflies (the same bits on every lane, so every branch is uniform); the full Newton
+// step once Armijo's decrease sinks under the objective's rounding.  The 1023-coalition sweep (config #2): 242 ms
+// (one 256-thread workgroup per coalition, serial factorisation) -> 2.2 ms (three 0.73 ms rounds;
+// profiles/r05_titanic_kernel_stats{,_rounds}.csv; per-phase times: scripts/lr_phases.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
+
 #include "keyed.h"
 #include "mplc_hip.h"
 
@@ -239,13 +242,17 @@ __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int
     const double dk = li < D ? b : 0.0;
     LR_PHASE(5);
     const double gd = wave_sum(lane < 32 ? gk * dk : 0.0);
-    // backtracking line search on the objective; the accepted value is the next iteration's f0
+    // backtracking line search on the objective; the accepted value is the next iteration's f0.  Near the optimum
+    // the Armijo decrease 1e-4 t g.d sinks under the rounding of the objective's row sum (~1e-14 |f|): no step
+    // could pass, and such fits used to spend their 100 iterations x 40 halvings stuck at |g| ~ 1e-9.  Once g.d <=
+    // 1e-10 |f| the full Newton step is taken (the quadratic-convergence region: |g| ~ 1e-5 for this problem).
+    const bool full = gd <= 1e-10 * fmax(1.0, fabs(f0));
     double t = 1.0, f1 = f0;
     for (int ls = 0; ls < 40; ++ls) {
       if (lane < D) sh.trial[lane] = sh.w[lane] - t * dk;
       __syncthreads();
       f1 = objective(sh.trial, rs, resident, X, Y, F, sh);
-      if (f1 <= f0 - 1e-4 * t * gd) break;
+      if (full || f1 <= f0 - 1e-4 * t * gd) break;
       t *= 0.5;
     }
     if (lane < D) sh.w[lane] = sh.trial[lane];
@@ -289,110 +296,207 @@ __device__ void lr_metrics(int n_correct, int n, double& loss, double& acc, doub
   acc = (double)n_correct / (double)n;
 }
 
-__global__ __launch_bounds__(LR_THREADS) void lr_fedavg_kernel(
-    const float* __restrict__ X, const float* __restrict__ Y, int F, const int32_t* __restrict__ rows,
-    const int32_t* __restrict__ rows_off, const int32_t* __restrict__ n_rows, const int32_t* __restrict__ splits,
-    int M, const uint64_t* __restrict__ masks, const uint64_t* __restrict__ keys, const double* __restrict__ agg_w,
-    const double* __restrict__ agg_scale, int epochs, int early_stopping, const float* __restrict__ Xv,
-    const float* __restrict__ Yv, int n_val, const float* __restrict__ Xt, const float* __restrict__ Yt, int n_test,
-    int32_t* __restrict__ correct, int32_t* __restrict__ epochs_done, double* __restrict__ theta_out,
-    double* __restrict__ hist, int64_t hist_stride) {
-  __shared__ Shared sh;
-  LR_PHASE(-1);
-  const int c = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int D = F + 1;
-  const uint64_t mask = masks[c];
-  const int P = __popcll(mask);  // partners in bit order (no per-lane array: it would live in scratch memory)
-  if (tid < LR_MAXF) { sh.theta[tid] = 0.0; sh.w[tid] = 0.0; sh.trial[tid] = 0.0; }
+// ------------------------------------------------------------------------------------------------
+// The FedAvg rounds as launches over all coalitions at once.  One coalition's rounds are a chain (each partner
+// fit warm-starts from the previous round's average), but within a round its |S| fits are independent: every
+// round is one launch whose waves take (coalition, partner) fits from a work queue, then one launch averages each
+// coalition's fits in partner order.  The sweep's length is then its total fit work over the machine plus one
+// round's longest fit per round, not its longest coalition's E x M x |S| chain of fits.
+// ------------------------------------------------------------------------------------------------
+constexpr int LR_HAVE = 1, LR_STOPPED = 2;  // coalition state bits: fitted global model / early-stopped
+
+struct LrJob {
+  const float* X;
+  const float* Y;
+  int F, M, C, epochs, early_stopping, n_val, n_test;
+  const int32_t* rows;
+  const int32_t* rows_off;
+  const int32_t* n_rows;
+  const int32_t* splits;
+  const uint64_t* masks;
+  const uint64_t* keys;
+  const double* agg_w;
+  const double* agg_scale;
+  const float* Xv;
+  const float* Yv;
+  const float* Xt;
+  const float* Yt;
+  double* hist;
+  int64_t hist_stride;
+  // workspace (one stream-ordered allocation per call)
+  double* theta;     // [C][LR_MAXF] the coalition's global model
+  double* wpart;     // [C][LR_MAXP][LR_MAXF] this round's partner fits
+  double* val_hist;  // [C][64] early stopping: val loss at each epoch's start
+  int32_t* item_off;  // [C + 1] first fit item of coalition c (exclusive prefix of |S|)
+  int32_t* state;     // [C] LR_HAVE | LR_STOPPED
+  int32_t* done;      // [C] epochs run
+  uint32_t* counters;  // [epochs * M] work-queue heads, one per round
+};
+
+__device__ __forceinline__ double* hist_row(const LrJob& j, int c, int e, int m) {
+  return j.hist + (int64_t)c * j.hist_stride + (int64_t)(e * j.M + m) * (2 + 4 * LR_MAXP);
+}
+
+// one block of 1024 threads: item offsets (exclusive prefix of the coalition sizes), state, queue heads
+__global__ __launch_bounds__(1024) void lr_prep_kernel(LrJob j) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (j.C + 1023) / 1024;
+  const int c0 = min(j.C, t * per), c1 = min(j.C, c0 + per);
+  int s = 0;
+  for (int c = c0; c < c1; ++c) s += __popcll(j.masks[c]);
+  part[t] = s;
   __syncthreads();
-  int done_epochs = epochs;
-  if (P == 1) {
-    // singleton: one fit on the partner's full data (E refits of the same rows reach the same optimum)
-    const int p = __builtin_ctzll(mask);
-    RowSel rs{rows, rows_off[p], n_rows[p], 0, n_rows[p], 0ull, false};
-    newton_fit(rs, X, Y, F, sh);
-    if (tid < D) theta_out[(int64_t)c * D + tid] = sh.w[tid];
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the 1024 chunk sums
+    const int v = t >= off ? part[t - off] : 0;
     __syncthreads();
-    if (hist) {  // SinglePartnerLearning logs its fit at [0, 0]
-      const int ct = count_correct_rows(sh.w, rs, X, Y, F);
-      const int cv = count_correct(sh.w, Xv, Yv, n_val, F);
-      if (tid == 0) {
-        double* h = hist + (int64_t)c * hist_stride + 2;
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = t ? part[t - 1] : 0;
+  for (int c = c0; c < c1; ++c) {
+    j.item_off[c] = run;
+    run += __popcll(j.masks[c]);
+  }
+  if (t == 1023) j.item_off[j.C] = part[1023];
+  for (int c = t; c < j.C; c += 1024) {
+    j.state[c] = 0;
+    j.done[c] = j.epochs;
+    j.val_hist[(int64_t)c * 64] = 0.0;  // epoch 0 starts unfitted: evaluate -> [0, 0]
+  }
+  for (int i = t; i < j.epochs * j.M; i += 1024) j.counters[i] = 0u;
+  if (j.hist && t < j.C) {  // round (0, 0) starts unfitted; a singleton has no collective entries
+    if (__popcll(j.masks[t]) > 1) hist_row(j, t, 0, 0)[0] = hist_row(j, t, 0, 0)[1] = 0.0;
+  }
+}
+
+// round (e, m): waves take (coalition, partner) fits from the round's queue until it is empty
+__global__ __launch_bounds__(LR_THREADS) void lr_fit_kernel(LrJob j, int e, int m) {
+  __shared__ Shared sh;
+  const int lane = threadIdx.x;
+  const int D = j.F + 1;
+  const int total = j.item_off[j.C];
+  uint32_t* head = j.counters + e * j.M + m;
+  if (lane < LR_MAXF) { sh.w[lane] = 0.0; sh.trial[lane] = 0.0; }
+  __syncthreads();
+  LR_PHASE(-1);
+  for (;;) {
+    int got = 0;
+    if (lane == 0) got = (int)atomicAdd(head, 1u);
+    const int item = __shfl(got, 0);
+    if (item >= total) break;  // every wave reaches this: the queue only grows past `total`
+    int lo = 0, hi = j.C - 1;  // the coalition: last c with item_off[c] <= item
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (j.item_off[mid] <= item) lo = mid;
+      else hi = mid - 1;
+    }
+    const int c = lo, pi = item - j.item_off[c];
+    const uint64_t mask = j.masks[c];
+    const int P = __popcll(mask);
+    const int st = j.state[c];
+    if (pi >= P || (st & LR_STOPPED) || (P == 1 && (e | m))) continue;  // a singleton fits once, in round (0, 0)
+    uint64_t rem = mask;
+    for (int k = 0; k < pi; ++k) rem &= rem - 1;
+    const int p = __builtin_ctzll(rem);
+    // singleton: one fit on the partner's full data (E refits of the same rows reach the same optimum)
+    const int* sp = j.splits + p * (j.M + 1);
+    const RowSel rs = P == 1 ? RowSel{j.rows, j.rows_off[p], j.n_rows[p], 0, j.n_rows[p], 0ull, false}
+                             : RowSel{j.rows, j.rows_off[p], j.n_rows[p], sp[m], sp[m + 1] - sp[m],
+                                      subkey(j.keys[(int64_t)c * LR_MAXP + pi], 0x10000u + (uint32_t)e, 0u), j.M > 1};
+    if (lane < D) sh.w[lane] = (st & LR_HAVE) ? j.theta[(int64_t)c * LR_MAXF + lane] : 0.0;  // warm start
+    __syncthreads();
+    LR_PHASE(10);
+    newton_fit(rs, j.X, j.Y, j.F, sh);
+    if (lane < D) j.wpart[((int64_t)c * LR_MAXP + pi) * LR_MAXF + lane] = sh.w[lane];
+    if (j.hist) {  // the partner's fit history: [loss, accuracy] on its rows, then on val (a singleton: round (0, 0))
+      const int ct = count_correct_rows(sh.w, rs, j.X, j.Y, j.F);
+      const int cv = count_correct(sh.w, j.Xv, j.Yv, j.n_val, j.F);
+      if (lane == 0) {
+        double* h = hist_row(j, c, e, m) + 2 + 4 * pi;
         lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
-        lr_metrics(cv, n_val, h[2], h[3], EPS_FITTED);
+        lr_metrics(cv, j.n_val, h[2], h[3], EPS_FITTED);
       }
     }
-  } else {
-    double* val_hist = sh.val_hist;
-    int have = 0;  // the initial model is unfitted (coef_ None): evaluate -> [0, 0]
-    for (int e = 0; e < epochs; ++e) {
-      if (early_stopping && epochs > 10 && e < 64) {
-        double vl = 0.0;
-        if (have) {  // log_loss(y, predict(x)) on hard 0/1 predictions, sklearn eps 1e-15
-          const int cv = count_correct(sh.theta, Xv, Yv, n_val, F);
-          const double eps = 1e-15;
-          vl = (double)(n_val - cv) * (-log(eps)) / (double)n_val + (double)cv * (-log(1.0 - eps)) / (double)n_val;
-        }
-        if (tid == 0) val_hist[e] = vl;
-        __syncthreads();
-      }
-      for (int m = 0; m < M; ++m) {
-        double* hrow = hist ? hist + (int64_t)c * hist_stride + (int64_t)(e * M + m) * (2 + 4 * LR_MAXP) : nullptr;
-        if (hrow) {  // the round-start collective model on val (eval_and_log_model_val_perf); unfitted: [0, 0]
-          const int cv = have ? count_correct(sh.theta, Xv, Yv, n_val, F) : 0;
-          if (tid == 0) {
-            if (have) lr_metrics(cv, n_val, hrow[0], hrow[1], EPS_GLOBAL);
-            else hrow[0] = hrow[1] = 0.0;
-          }
-        }
-        if (tid < D) sh.acc[tid] = 0.0;
-        __syncthreads();
-        uint64_t rem = mask;
-        for (int pi = 0; pi < P; ++pi, rem &= rem - 1) {
-          const int p = __builtin_ctzll(rem);
-          const int* sp = splits + p * (M + 1);
-          RowSel rs{rows, rows_off[p], n_rows[p], sp[m], sp[m + 1] - sp[m],
-                    subkey(keys[(int64_t)c * LR_MAXP + pi], 0x10000u + (uint32_t)e, 0u), M > 1};
-          if (tid < D) sh.w[tid] = have ? sh.theta[tid] : 0.0;  // warm start from the global model
-          __syncthreads();
-          LR_PHASE(10);
-          newton_fit(rs, X, Y, F, sh);
-          if (hrow) {  // the partner's fit history: [loss, accuracy] on its minibatch, then on val
-            const int ct = count_correct_rows(sh.w, rs, X, Y, F);
-            const int cv = count_correct(sh.w, Xv, Yv, n_val, F);
-            if (tid == 0) {
-              double* h = hrow + 2 + 4 * pi;
-              lr_metrics(ct, rs.count, h[0], h[1], EPS_FITTED);
-              lr_metrics(cv, n_val, h[2], h[3], EPS_FITTED);
-            }
-          }
-          // np.average: multiply then sum in partner order (float64)
-          if (tid < D) {
-            const double prod = sh.w[tid] * agg_w[(int64_t)c * LR_MAXP + pi];
-            sh.acc[tid] = (pi == 0) ? prod : sh.acc[tid] + prod;
-          }
-          __syncthreads();
-        }
-        if (tid < D) sh.theta[tid] = sh.acc[tid] / agg_scale[c];
-        LR_PHASE(8);
-        have = 1;
-        __syncthreads();
-      }
-      if (early_stopping && epochs > 10 && e >= 10 && e < 64 && val_hist[e] > val_hist[e - 10]) {
-        done_epochs = e + 1;
-        break;
-      }
-    }
-    if (tid < D) theta_out[(int64_t)c * D + tid] = sh.theta[tid];
-    if (tid < D) sh.w[tid] = sh.theta[tid];
     __syncthreads();
   }
   LR_PHASE(7);
-  const int cc = count_correct(sh.w, Xt, Yt, n_test, F);
-  if (tid == 0) {
+}
+
+// round (e, m), one wave per coalition: np.average of the partner fits (multiply, then sum in partner order, fp64);
+// at an epoch's end the early-stopping test (mplc/multi_partner_learning.py:177-193: round-0 val loss of epoch e
+// against e - 10), then the next round's start values from the new global model
+__global__ __launch_bounds__(LR_THREADS) void lr_avg_kernel(LrJob j, int e, int m) {
+  __shared__ double th[LR_MAXF];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int D = j.F + 1;
+  const int st = j.state[c];
+  if (st & LR_STOPPED) return;
+  const int P = __popcll(j.masks[c]);
+  double* theta = j.theta + (int64_t)c * LR_MAXF;
+  const double* wp = j.wpart + (int64_t)c * LR_MAXP * LR_MAXF;
+  if (P == 1) {
+    if (e == 0 && m == 0) {
+      if (lane < D) theta[lane] = wp[lane];
+      if (lane == 0) j.state[c] = LR_HAVE;
+    }
+    return;
+  }
+  if (lane < LR_MAXF) {
+    // numpy multiplies, then adds: no fused multiply-add here (tests/test_lr.py pins it bit for bit)
+#pragma clang fp contract(off)
+    double acc = 0.0;
+    if (lane < D) {
+      for (int pi = 0; pi < P; ++pi) {
+        const double prod = wp[pi * LR_MAXF + lane] * j.agg_w[(int64_t)c * LR_MAXP + pi];
+        acc = (pi == 0) ? prod : acc + prod;
+      }
+      acc = acc / j.agg_scale[c];
+      theta[lane] = acc;
+    }
+    th[lane] = acc;
+  }
+  __syncthreads();
+  int state = LR_HAVE;
+  double* vh = j.val_hist + (int64_t)c * 64;
+  const bool es = j.early_stopping && j.epochs > 10;
+  if (es && m == j.M - 1 && e >= 10 && e < 64 && vh[e] > vh[e - 10]) {
+    state |= LR_STOPPED;
+    if (lane == 0) j.done[c] = e + 1;
+  }
+  const int en = (m + 1 < j.M) ? e : e + 1, mn = (m + 1 < j.M) ? m + 1 : 0;  // the next round
+  if (!(state & LR_STOPPED) && en < j.epochs) {
+    if (es && mn == 0 && en < 64) {  // log_loss(y, predict(x)) on hard 0/1 predictions, sklearn eps 1e-15
+      const int cv = count_correct(th, j.Xv, j.Yv, j.n_val, j.F);
+      const double eps = 1e-15;
+      if (lane == 0)
+        vh[en] = (double)(j.n_val - cv) * (-log(eps)) / (double)j.n_val + (double)cv * (-log(1.0 - eps)) / (double)j.n_val;
+    }
+    if (j.hist) {  // the round-start collective model on val (eval_and_log_model_val_perf)
+      const int cv = count_correct(th, j.Xv, j.Yv, j.n_val, j.F);
+      if (lane == 0) {
+        double* h = hist_row(j, c, en, mn);
+        lr_metrics(cv, j.n_val, h[0], h[1], EPS_GLOBAL);
+      }
+    }
+  }
+  if (lane == 0) j.state[c] = state;
+}
+
+// the final model of every coalition: theta_out, test hits, epochs run
+__global__ __launch_bounds__(LR_THREADS) void lr_final_kernel(LrJob j, int32_t* __restrict__ correct,
+                                                              int32_t* __restrict__ epochs_done,
+                                                              double* __restrict__ theta_out) {
+  __shared__ double th[LR_MAXF];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int D = j.F + 1;
+  if (lane < LR_MAXF) th[lane] = lane < D ? j.theta[(int64_t)c * LR_MAXF + lane] : 0.0;
+  __syncthreads();
+  if (lane < D) theta_out[(int64_t)c * D + lane] = th[lane];
+  const int cc = count_correct(th, j.Xt, j.Yt, j.n_test, j.F);
+  if (lane == 0) {
     correct[c] = cc;
-    epochs_done[c] = done_epochs;
+    epochs_done[c] = j.done[c];
   }
 }
 
@@ -415,10 +519,42 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
       n_test < 1)
     return MPLC_E_ARG;
   if (early_stopping && (!x_val || !y_val || n_val < 1)) return MPLC_E_ARG;
-  lr_fedavg_kernel<<<n_coalitions, LR_THREADS, 0, (hipStream_t)stream>>>(
-      x, y, n_features, rows, rows_off, n_rows, splits, minibatch_count, masks, keys, agg_w, agg_scale, epochs,
-      early_stopping, x_val, y_val, n_val, x_test, y_test, n_test, correct, epochs_done, theta_out, hist,
-      hist_stride);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? MPLC_OK : (int)e;
+  if (hist && n_coalitions > 1024) return MPLC_E_ARG;  // the history is for single coalitions
+  const int64_t C = n_coalitions, R = (int64_t)epochs * minibatch_count;
+  if (R > (1 << 20)) return MPLC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t b_theta = (size_t)C * LR_MAXF * 8, b_wpart = (size_t)C * LR_MAXP * LR_MAXF * 8,
+               b_vh = (size_t)C * 64 * 8, b_off = (size_t)(C + 1) * 4, b_st = (size_t)C * 4, b_ctr = (size_t)R * 4;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bytes = up(b_theta) + up(b_wpart) + up(b_vh) + up(b_off) + 2 * up(b_st) + up(b_ctr);
+  char* ws = nullptr;
+  hipError_t err = hipMallocAsync((void**)&ws, bytes, s);
+  if (err != hipSuccess) return (int)err;
+  LrJob j{};
+  j.X = x, j.Y = y, j.F = n_features, j.M = minibatch_count, j.C = n_coalitions, j.epochs = epochs;
+  j.early_stopping = early_stopping, j.n_val = n_val, j.n_test = n_test;
+  j.rows = rows, j.rows_off = rows_off, j.n_rows = n_rows, j.splits = splits, j.masks = masks, j.keys = keys;
+  j.agg_w = agg_w, j.agg_scale = agg_scale, j.Xv = x_val, j.Yv = y_val, j.Xt = x_test, j.Yt = y_test;
+  j.hist = hist, j.hist_stride = hist_stride;
+  char* q = ws;
+  j.theta = (double*)q, q += up(b_theta);
+  j.wpart = (double*)q, q += up(b_wpart);
+  j.val_hist = (double*)q, q += up(b_vh);
+  j.item_off = (int32_t*)q, q += up(b_off);
+  j.state = (int32_t*)q, q += up(b_st);
+  j.done = (int32_t*)q, q += up(b_st);
+  j.counters = (uint32_t*)q;
+  lr_prep_kernel<<<1, 1024, 0, s>>>(j);
+  // the fit launches' persistent grid: 4 one-wave workgroups per CU (the LDS of Shared) fill the 256 CUs
+  const int grid = (int)std::min<int64_t>(C * LR_MAXP, 1024);
+  for (int e = 0; e < epochs; ++e)
+    for (int m = 0; m < minibatch_count; ++m) {
+      lr_fit_kernel<<<grid, LR_THREADS, 0, s>>>(j, e, m);
+      lr_avg_kernel<<<n_coalitions, LR_THREADS, 0, s>>>(j, e, m);
+    }
+  lr_final_kernel<<<n_coalitions, LR_THREADS, 0, s>>>(j, correct, epochs_done, theta_out);
+  err = hipGetLastError();
+  const hipError_t ferr = hipFreeAsync(ws, s);
+  if (err != hipSuccess) return (int)err;
+  return ferr == hipSuccess ? MPLC_OK : (int)ferr;
 }

@@ -92,7 +92,10 @@ int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, const int32_t* 
                                      int64_t out_stride, int64_t skip_lo, int64_t skip_hi, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
- * Batched FedAvg logistic regression (Titanic model, BASELINE config #2), one workgroup per coalition.
+ * Batched FedAvg logistic regression (Titanic model, BASELINE config #2), all coalitions at once: per FedAvg
+ * round one launch whose waves take (coalition, partner) fits from a work queue and one launch that averages
+ * each coalition's fits; a stream-ordered workspace (hipMallocAsync / hipFreeAsync on `stream`) holds the
+ * coalitions' models between the launches.
  * Replaces, per coalition, FederatedAverageLearning.fit (mplc/multi_partner_learning.py:195-216,
  * 285-334) with the Titanic.LogisticRegression model (mplc/dataset.py:323-394: sklearn L2 LR, C=1),
  * np.average aggregation (mplc/mpl_utils.py:90-115) and the test accuracy (:158-169).  Every fit is the

@@ -112,6 +112,32 @@ def test_titanic_exact_shapley_all_1023_coalitions():
 
 
 @pytest.mark.gpu
+def test_fedavg_round_is_np_average_of_the_partner_fits():
+    """E = 1, M = 1: a coalition's round-0 fits are its partners' singleton fits (same rows, same zero start, same
+    code), so its model must be np.average of the singletons' models with the reference's weights, bit for bit
+    (mplc/mpl_utils.py:90-115: multiply, then sum in partner order - no fused multiply-add)."""
+    from itertools import combinations
+
+    from mplc.dataset import Titanic
+    from mplc.engine import CoalitionEngine
+    from mplc.fedavg import aggregation_weights
+    from mplc.scenario import Scenario
+    sc = Scenario(10, [0.1] * 10, dataset=Titanic(synthetic=True), epoch_count=1, minibatch_count=1,
+                  is_early_stopping=False).provision()
+    eng = CoalitionEngine.for_scenario(sc)
+    singles = [(p,) for p in range(10)]
+    coals = singles + [c for k in (2, 3, 5, 10) for c in combinations(range(10), k)][::7]
+    eng.evaluate(coals)
+    theta = eng.last_theta
+    sizes = eng.partner_sizes
+    for ci, c in enumerate(coals[10:], start=10):
+        w, scl = aggregation_weights([sizes[p] for p in c])
+        wgt = np.asarray(w, dtype=np.float64).reshape(-1, 1)
+        want = np.multiply(np.array([theta[p] for p in c]), wgt).sum(axis=0) / scl
+        assert np.array_equal(theta[ci], want), (c, np.abs(theta[ci] - want).max())
+
+
+@pytest.mark.gpu
 def test_lr_history_matches_reference(golden):
     """The grand coalition's learning history (mplc/mpl_utils.py:11-27) against the reference's own
     (tests/golden/lr_history.json: FederatedAverageLearning with Titanic.LogisticRegression on the same
