@@ -181,22 +181,25 @@ class Contributivity:
 
     def not_twice_characteristic(self, subset):
         """Memoised v(S) plus the increment bookkeeping of mplc/contributivity.py:92-136."""
-        subset = np.asarray(subset)
-        key = tuple(int(i) for i in np.sort(subset)) if len(subset) > 0 else ()
+        key = tuple(sorted(int(i) for i in subset))
         values = self.charac_fct_values
         if key not in values:
             self.first_charac_fct_calls_count += 1
-            values[key] = self._coalition_value(key)
-            members = set(key)
+            v = values[key] = self._coalition_value(key)
+            inc = self.increments_values
+            # the reference's loop over i in 0..n-1 (same order, same keys and values): a member's key without it
+            # is key minus one slot; a non-member's key with it is key with i inserted at its sorted position
+            pos = 0  # members of key below i
             for i in range(self._n):
-                if i in members:
-                    without = tuple(j for j in key if j != i)
+                if pos < len(key) and key[pos] == i:
+                    without = key[:pos] + key[pos + 1:]
                     if without in values:
-                        self.increments_values[i][without] = values[key] - values[without]
+                        inc[i][without] = v - values[without]
+                    pos += 1
                 else:
-                    with_i = tuple(sorted(key + (i,)))
+                    with_i = key[:pos] + (i,) + key[pos:]
                     if with_i in values:
-                        self.increments_values[i][key] = values[with_i] - values[key]
+                        inc[i][key] = values[with_i] - v
         return values[key]
 
     # --------------------------------------------------------------------------------------------
