@@ -1389,10 +1389,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int TY = (HOV + 1) / 2, TX = (WOV + 1) / 2;
   constexpr int NB = (TY + BTY - 1) / BTY;
   constexpr int LR = 2 * BTY + 2, LC = 2 * TX + 2;
-  constexpr int CIP = CIB + 1;
+  // channel strides padded by 8 (not 1): a half-wave reads 16 channels (tl) of 2 adjacent tiles (kq), 2 CIP apart;
+  // 2 CIP = 16 (mod 32) puts the two tiles on opposite halves of the 32 banks (CIB + 1 gave 2-way conflicts):
+  // conv2 / conv4 weight gradients -2.5 % / -2.7 %, bit-identical (profiles/r05_ab_wgrad_lds_pad.txt)
+  constexpr int CIP = CIB + 8;
   constexpr int XROW = LC * CIP;
   constexpr int ZR = 2 * BTY, ZC = 2 * TX;
-  constexpr int COP = CO + 1;
+  constexpr int COP = CO + 8;
   constexpr int NH = CIB / 16, NCG = CO / 16;
   constexpr int XS = LR * XROW, ZS = ZR * ZC * COP;
   constexpr int PS = 4 * 3 * 16 * CO;  // the four waves' P_i for 16 input channels
@@ -2271,9 +2274,9 @@ __global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict_
 #define CONV4_DGRAD wino_kernel<13, 13, 64, 64, 2, 4, EPI_BWD_MASK, 1>   /* 8x8 tiles,    2 bands, 63.7 KB */
 #define CONV1_WGRAD wgrad_kernel<32, 32, 3, 32, 1, 32, 32, 8, 4>
 // Winograd F(3x3,2x2) weight gradients: <HI, WI, CI, CO, PAD, HOV, WOV, tile rows per band, ci per block>
-#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1, 0>  /* 15x15 tiles, 5 bands, 56.9 KB */
-#define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 57.1 KB */
-#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1, 1>  /* 6x6 tiles, 1 band, 2 ci chunks */
+#define CONV2_WGRAD wino_wgrad_kernel<32, 32, 32, 32, 0, 30, 30, 3, 32, 1, 0>  /* 15x15 tiles, 5 bands, 73.9 KB */
+#define CONV3_WGRAD wino_wgrad_kernel<15, 15, 32, 64, 1, 15, 15, 4, 32>  /* 8x8 tiles,   2 bands, 69.8 KB */
+#define CONV4_WGRAD wino_wgrad_kernel<15, 15, 64, 64, 0, 12, 12, 6, 32, 1, 1>  /* 6x6 tiles, 1 band, 2 ci chunks, 76.9 KB */
 // dz2 / dz4 slots hold the pooled gradients: conv3's data gradient (out [15][15][32]) and dense5_bwd write them,
 // conv2's / conv4's data (UPI: in [HI/2][WI/2][CI]) and weight (UPZ: dz [HO/2][WO/2][CO]) gradients read them
 static_assert(15 * 15 * 32 == MPLC_CIFAR_DZ2 && (30 / 2) * (30 / 2) * 32 == MPLC_CIFAR_DZ2, "dz2 slot stride");
