@@ -150,7 +150,8 @@ constexpr int FWD_C1R = 2 * FWD_PR + 2;            // conv1 rows per block
 constexpr int FWD_IMR = FWD_C1R + 2;               // image rows per block
 constexpr int FWD_C1T = (FWD_C1R * A1 + 31) / 32;  // conv1 tiles (9)
 constexpr int FWD_TILES = FWD_PR * PL;             // 48 Winograd tiles (= pool windows) per block
-constexpr int FWD_TS = C2 + 1;                     // tile stride of a T plane (odd: conflict-free writes)
+constexpr int FWD_TS = C2 + 4;  // tile stride of a T plane: a half-wave writes tile quads kq, kq + 1 (4 TS apart) on opposite
+                                // bank halves (4 TS = 16 mod 32; 65 gave 2-way conflicts): -1.5 %, bit-identical
 constexpr int FWD_TQ = 16 * FWD_TS;                // one (row i, b) plane of T for a 16-tile group
 constexpr int FWD_NIT = (FWD_IMR * IMG + FWD_THREADS - 1) / FWD_THREADS;  // image values per thread
 constexpr int FWD_SPB = 9;  // samples per block (config #3's bs 27 = 3 groups; 3: +1 %, 14 / 27: +1.2 % / +3 %)
