@@ -137,6 +137,69 @@ def test_fedavg_round_is_np_average_of_the_partner_fits():
         assert np.array_equal(theta[ci], want), (c, np.abs(theta[ci] - want).max())
 
 
+def _restated_fedavg(sc, eng, coal, E, M, es, n_val):
+    """Host restatement of the device FedAvg with minibatches and the early-stopping rule (mplc/multi_partner_learning.py
+    :177-193, 285-334): each round every partner's exact fit (oracle/lr.py) on its minibatch of the keyed epoch
+    permutation, np.average with data-volume weights; val loss of the round-0 model of each epoch on hard predictions
+    (sklearn eps 1e-15), stop after epoch e >= 10 when it exceeds epoch e - 10's."""
+    from mplc.cnn import keyed_perm, minibatch_bounds, shuffle_key, subkey
+    from mplc.fedavg import aggregation_weights
+    parts = [(np.asarray(p.x_train, dtype=np.float64), np.asarray(p.y_train)) for p in sc.partners_list]
+    xv, yv = np.asarray(sc.dataset.x_val, dtype=np.float64), np.asarray(sc.dataset.y_val)
+    mask = sum(1 << p for p in coal)
+    w, scl = aggregation_weights([len(parts[p][1]) for p in coal])
+    theta, have, vh, done = None, False, [], E
+    for e in range(E):
+        if es and E > 10 and e < 64:
+            if have:
+                cv = int(round(olr.accuracy(theta, xv, yv) * len(yv)))
+                vh.append(((n_val - cv) * -np.log(1e-15) + cv * -np.log(1 - 1e-15)) / n_val)
+            else:
+                vh.append(0.0)
+        for m in range(M):
+            fits = []
+            for p in coal:
+                n_p = len(parts[p][1])
+                sp = minibatch_bounds(n_p, M)
+                key = subkey(shuffle_key(eng.seed, mask, p), 0x10000 + e, 0)
+                pos = [keyed_perm(key, n_p, i) if M > 1 else i for i in range(sp[m], sp[m + 1])]
+                fits.append(olr.fit_exact(parts[p][0][pos], parts[p][1][pos]))
+            theta = np.multiply(np.array(fits), np.asarray(w).reshape(-1, 1)).sum(axis=0) / scl
+            have = True
+        if es and E > 10 and 10 <= e < 64 and vh[e] > vh[e - 10]:
+            done = e + 1
+            break
+    return theta, done
+
+
+@pytest.mark.gpu
+def test_device_lr_minibatches_and_early_stopping_vs_restatement(golden):
+    """M = 3 (the keyed per-epoch permutation, np.split bounds) and E = 14 with the early-stopping rule, on the
+    reference's 5-partner Titanic case: thetas within 1e-8 of the host restatement, the same stop epochs and
+    test accuracies."""
+    case = [c for c in golden["cases"] if c["partners_count"] == 5][0]
+    from mplc.dataset import Titanic
+    from mplc.engine import CoalitionEngine
+    from mplc.scenario import Scenario
+    X = np.array(golden["data"]["X"], dtype=np.float32)
+    y = np.array(golden["data"]["y"], dtype=np.float32)
+    E, M = 14, 3
+    sc = Scenario(5, case["amounts"], dataset=Titanic(x=X, y=y), epoch_count=E, minibatch_count=M,
+                  is_early_stopping=True).provision()
+    eng = CoalitionEngine.for_scenario(sc)
+    coals = [(0, 1), (1, 3), (0, 2, 4), (1, 2, 3, 4), (0, 1, 2, 3, 4)]
+    res = eng.evaluate(coals, return_details=True, is_early_stopping=True)
+    n_val = len(sc.dataset.y_val)
+    stops = []
+    for ci, c in enumerate(coals):
+        theta, done = _restated_fedavg(sc, eng, c, E, M, True, n_val)
+        stops.append(done)
+        assert res["epochs_done"][ci] == done, (c, res["epochs_done"][ci], done)
+        assert np.max(np.abs(eng.last_theta[ci] - theta)) < 1e-8, (c, np.max(np.abs(eng.last_theta[ci] - theta)))
+        assert res["scores"][ci] == olr.accuracy(theta, sc.dataset.x_test, sc.dataset.y_test)
+    print("stop epochs", stops)
+
+
 @pytest.mark.gpu
 def test_lr_history_matches_reference(golden):
     """The grand coalition's learning history (mplc/mpl_utils.py:11-27) against the reference's own
