@@ -181,7 +181,10 @@ class Contributivity:
 
     def not_twice_characteristic(self, subset):
         """Memoised v(S) plus the increment bookkeeping of mplc/contributivity.py:92-136."""
-        key = tuple(sorted(int(i) for i in subset))
+        return self._not_twice_key(tuple(sorted(int(i) for i in subset)))
+
+    def _not_twice_key(self, key):
+        """not_twice_characteristic for a key already in normal form (a sorted tuple of ints)."""
         values = self.charac_fct_values
         if key not in values:
             self.first_charac_fct_calls_count += 1
@@ -229,9 +232,9 @@ class Contributivity:
         self._begin()
         logger.info("# Launching computation of Shapley Value of all partners")
         n = self._n
-        coalitions = [list(c) for r in range(1, n + 1) for c in combinations(range(n), r)]
+        coalitions = [c for r in range(1, n + 1) for c in combinations(range(n), r)]  # sorted int tuples
         self.prefetch(coalitions)
-        char_values = [self.not_twice_characteristic(c) for c in coalitions]
+        char_values = [self._not_twice_key(c) for c in coalitions]
         # every rank holds the same (all-reduced) values here, so the sum may be range-sharded across them
         sv = shapley_value(n, char_values, sharded=True)
         self.name = "Shapley"

@@ -26,11 +26,12 @@ def coalition_tables(coalitions, partner_sizes, seed, aggregation):
     the per-coalition loop (tests/test_lr.py); the loop cost about 35 ms per 1023-coalition sweep on the host."""
     C = len(coalitions)
     n = len(partner_sizes)
+    lens = np.fromiter((len(c) for c in coalitions), dtype=np.int64, count=C)
+    flat = np.fromiter((p for c in coalitions for p in c), dtype=np.int64, count=int(lens.sum()))
+    if np.any(lens > MAXP) or (len(flat) and (flat.min() < 0 or flat.max() >= n)):
+        raise ValueError("invalid coalition: more than 64 partners or a partner id out of range")
     member = np.zeros((C, n), dtype=bool)
-    for ci, c in enumerate(coalitions):
-        if len(c) > MAXP or (len(c) and c[-1] >= n):
-            raise ValueError(f"invalid coalition {c}")
-        member[ci, list(c)] = True
+    member[np.repeat(np.arange(C), lens), flat] = True
     bits = np.left_shift(np.uint64(1), np.arange(n, dtype=np.uint64))
     masks = (member * bits).sum(axis=1, dtype=np.uint64)
     counts = member.sum(axis=1)
