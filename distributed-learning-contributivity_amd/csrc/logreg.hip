@@ -17,9 +17,10 @@
 // column 31); lane i factorises row i of H in registers (right-looking Cholesky, multipliers broadcast with
 // v_readlane, the padding rows set to the identity so no loop needs a data-dependent guard); the solves on the
 // lanes; wave sums as xor butterflies (the same bits on every lane, so every branch is uniform); the full Newton
-// step once Armijo's decrease sinks under the objective's rounding.  The 1023-coalition sweep (config #2): 242 ms
-// (one 256-thread workgroup per coalition, serial factorisation) -> 2.2 ms (three 0.73 ms rounds;
-// profiles/r05_titanic_kernel_stats{,_rounds}.csv; per-phase times: scripts/lr_phases.py).
+// step once Armijo's decrease sinks under the objective's rounding; two waves per SIMD (19 KB of LDS: the rows staged
+// as their fp32 values, 64 at a time).  The 1023-coalition sweep (config #2): 242 ms (one 256-thread workgroup per
+// coalition, serial factorisation) -> 1.7 ms (three 0.56 ms rounds; profiles/r05_titanic_kernel_stats{,_rounds,
+// _occ2}.csv; per-phase times: scripts/lr_phases.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,22 +39,21 @@ namespace {
 constexpr int LR_THREADS = 64;   // one wave per coalition
 constexpr int LR_MAXF = 32;      // D = n_features + 1 unknowns (coef | intercept) supported
 constexpr int LR_MAXP = 64;      // partners per coalition
-constexpr int LR_NMAX = 96;      // rows staged in LDS at a time (a whole Titanic fit: <= 71 rows)
-constexpr int LR_XS = LR_MAXF + 2;  // staged row stride in doubles: 16-byte aligned rows, 4-way banked per-lane reads
+constexpr int LR_NMAX = 64;      // rows staged in LDS at a time (config #2's fits: 56-57 rows; larger fits stream)
+constexpr int LR_XS = LR_MAXF + 1;  // staged row stride in floats (odd: per-lane row reads 2-way banked)
 constexpr int LR_LS = LR_MAXF + 1;  // row stride of the Hessian / factor in LDS: lane li's row reads 2-way banked
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// 19.3 KB: two one-wave workgroups per SIMD fit a CU's 160 KB of LDS
 struct Shared {
-  double theta[LR_MAXF];
   double w[LR_MAXF];       // current Newton iterate (entries >= D stay 0)
   double trial[LR_MAXF];   // line-search trial point (entries >= D stay 0)
-  double acc[LR_MAXF];     // FedAvg accumulator
   double L[LR_MAXF * LR_LS];  // the Hessian's tiles, then the Cholesky factor (row-major, stride LR_LS)
   double hv[LR_NMAX];      // s (1 - s) of the staged rows, s = sigma(-y z)
   double sv[LR_NMAX];      // -y s
-  double xs[LR_NMAX * LR_XS];  // staged rows [i][k]: features k < F, 1 at k = F (the intercept's column), 0 after
-  double ys[LR_NMAX];      // +-1
-  double val_hist[64];
+  float xs[LR_NMAX * LR_XS];  // staged rows [i][k] (the data's fp32): features k < F, 1 at k = F (intercept), 0 after
+  float ys[LR_NMAX];       // +-1
+  int rid[LR_NMAX];
 };
 
 // Sum over the wave: an xor butterfly, so every lane ends with the same bits (each level adds the same two
@@ -92,27 +92,29 @@ struct RowSel {
 // rows [c0, c0 + cn) of the fit into LDS as fp64 (exact widening of the fp32 data), the intercept's column of ones
 // and zero padding appended, labels as +-1
 __device__ void stage_rows(const RowSel& rs, int c0, int cn, const float* X, const float* Y, int F, Shared& sh) {
-  // lanes over rows: each lane gathers its row's F features with independent loads (one memory latency per row,
-  // not one per feature)
-  for (int i = threadIdx.x; i < cn; i += LR_THREADS) {
+  const int lane = threadIdx.x;
+  for (int i = lane; i < cn; i += LR_THREADS) {
     const int r = rs.row(c0 + i);
-    sh.ys[i] = Y[r] > 0.5f ? 1.0 : -1.0;
-    const float* xr = X + (int64_t)r * F;
-    double* dst = sh.xs + i * LR_XS;
-    float v[LR_MAXF];
-#pragma unroll
-    for (int k = 0; k < LR_MAXF; ++k) v[k] = xr[min(k, F - 1)];  // unconditional: the loads issue back to back
-#pragma unroll
-    for (int k = 0; k < LR_MAXF; ++k) dst[k] = k < F ? (double)v[k] : (k == F ? 1.0 : 0.0);
+    sh.rid[i] = r;
+    sh.ys[i] = Y[r] > 0.5f ? 1.0f : -1.0f;
+  }
+  __syncthreads();
+  // (row, column) pairs over the lanes, 32 columns a row: no per-column address table for the compiler to keep
+  // live across the kernel (an unrolled per-lane row loop held 32 offsets and 32 masks in registers)
+#pragma unroll 4
+  for (int e = lane; e < cn * LR_MAXF; e += LR_THREADS) {
+    const int i = e >> 5, k = e & (LR_MAXF - 1);
+    const float v = X[(int64_t)sh.rid[i] * F + min(k, F - 1)];
+    sh.xs[i * LR_XS + k] = k < F ? v : (k == F ? 1.0f : 0.0f);
   }
   __syncthreads();
 }
 
 // w . [x | 1] over a staged row (w's entries >= D are 0, as are the row's)
-__device__ __forceinline__ double row_z(const double* w, const double* xr) {
+__device__ __forceinline__ double row_z(const double* w, const float* xr) {
   double z = 0.0;
 #pragma unroll
-  for (int k = 0; k < LR_MAXF; ++k) z += w[k] * xr[k];
+  for (int k = 0; k < LR_MAXF; ++k) z += w[k] * (double)xr[k];
   return z;
 }
 
@@ -125,7 +127,7 @@ __device__ double objective(const double* w, const RowSel& rs, bool resident, co
     const int cn = min(LR_NMAX, rs.count - c0);
     if (!resident) stage_rows(rs, c0, cn, X, Y, F, sh);
     for (int i = lane; i < cn; i += LR_THREADS) {
-      const double t = -sh.ys[i] * row_z(w, sh.xs + i * LR_XS);
+      const double t = -(double)sh.ys[i] * row_z(w, sh.xs + i * LR_XS);
       part += t > 0 ? t + log1p(exp(-t)) : log1p(exp(t));
     }
     if (!resident) __syncthreads();
@@ -160,7 +162,7 @@ __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int
       for (int i = lane; i < cn4; i += LR_THREADS) {  // per row: s = sigma(-y z), s (1 - s); 0 on the padding
         double sv = 0.0, hv = 0.0;
         if (i < cn) {
-          const double yy = sh.ys[i];
+          const double yy = (double)sh.ys[i];
           const double sg = 1.0 / (1.0 + exp(yy * row_z(sh.w, sh.xs + i * LR_XS)));
           sv = -yy * sg;
           hv = sg * (1.0 - sg);
@@ -172,8 +174,8 @@ __device__ void newton_fit(const RowSel& rs, const float* X, const float* Y, int
       for (int r0 = 0; r0 < cn; r0 += 4) {
         const int r = r0 + kk;
         const bool ok = r < cn;
-        const double a0 = ok ? sh.xs[r * LR_XS + idx] : 0.0;
-        const double a1 = ok ? sh.xs[r * LR_XS + 16 + idx] : 0.0;
+        const double a0 = ok ? (double)sh.xs[r * LR_XS + idx] : 0.0;
+        const double a1 = ok ? (double)sh.xs[r * LR_XS + 16 + idx] : 0.0;
         const double hr = sh.hv[r];
         const double b0 = hr * a0;
         const double b1 = idx == 15 ? sh.sv[r] : hr * a1;
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(1024) void lr_prep_kernel(LrJob j) {
 }
 
 // round (e, m): waves take (coalition, partner) fits from the round's queue until it is empty
-__global__ __launch_bounds__(LR_THREADS) void lr_fit_kernel(LrJob j, int e, int m) {
+__global__ __launch_bounds__(LR_THREADS, 2) void lr_fit_kernel(LrJob j, int e, int m) {
   __shared__ Shared sh;
   const int lane = threadIdx.x;
   const int D = j.F + 1;
@@ -545,8 +547,8 @@ extern "C" int mplc_lr_fedavg(const float* x, const float* y, int n_features, co
   j.done = (int32_t*)q, q += up(b_st);
   j.counters = (uint32_t*)q;
   lr_prep_kernel<<<1, 1024, 0, s>>>(j);
-  // the fit launches' persistent grid: 4 one-wave workgroups per CU (the LDS of Shared) fill the 256 CUs
-  const int grid = (int)std::min<int64_t>(C * LR_MAXP, 1024);
+  // the fit launches' persistent grid: 8 one-wave workgroups per CU (2 per SIMD) on the 256 CUs
+  const int grid = (int)std::min<int64_t>(C * LR_MAXP, 2048);
   for (int e = 0; e < epochs; ++e)
     for (int m = 0; m < minibatch_count; ++m) {
       lr_fit_kernel<<<grid, LR_THREADS, 0, s>>>(j, e, m);
