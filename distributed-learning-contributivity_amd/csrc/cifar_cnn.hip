@@ -1738,6 +1738,88 @@ __global__ __launch_bounds__(256) void dense5_fwd_kernel(const float* __restrict
   }
 }
 
+// The same Dense(512) forward in blocks of 16 samples x 64 columns on v_mfma_f32_16x16x4f32 (wave = 16 columns):
+// at TMCS batch sizes (15-16 samples per replica) one m-tile without idle rows, and twice the waves of the 32 x 128
+// form streaming W5: -13 % at 260 replicas, -18 % at 140 (profiles/r05_ab_dense5_fwd16.txt).  Bit-identical to it:
+// both matrix-core forms accumulate each output as the fmaf chain over k in order.  Launched for
+// B <= MPLC_D5F16_MAX slots; larger B (the evaluation's sample chunks) keeps the 32-row form, which reads W5 half as
+// often.  The variant library (build_native.VARIANTS, MPLC_D5F16_MAX=0) runs the 32-row form everywhere, and
+// tests/test_variants_gpu.py holds the two to the same bits.
+#ifndef MPLC_D5F16_MAX
+#define MPLC_D5F16_MAX 16
+#endif
+__global__ __launch_bounds__(256) void dense5_fwd16_kernel(const float* __restrict__ A, const int32_t* __restrict__ cnt,
+                                                           int cnt_all, int bmax, const float* __restrict__ params,
+                                                           int64_t stride, const float* __restrict__ glob,
+                                                           const int32_t* __restrict__ w5src,
+                                                           const uint64_t* __restrict__ drop_key,
+                                                           float* __restrict__ H, uint8_t* __restrict__ code) {
+  __shared__ float a_s[16 * (DF_K + 1)];
+  const LogicalBlock lbk = xcd_block3();  // (sample tile, column slice, replica): a replica's W5 in one XCD's L2
+  const int r = lbk.z;
+  const int m0 = lbk.x * 16;
+  const int count = cnt ? cnt[r] : cnt_all;
+  if (m0 >= count) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n0 = lbk.y * 64 + wave * 16;
+  const int tl = lane & 15, kq = lane >> 4;
+  const float* Ar = A + (int64_t)r * bmax * FEAT;
+  const int gsrc = w5src ? w5src[r] : -1;
+  const float* W = (gsrc >= 0 ? glob + (int64_t)gsrc * stride : params + (int64_t)r * stride) + OFF_W5;
+  fvec4 acc = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+  constexpr int AIT = 16 * DF_K / 256;
+  const float* wl = W + n0 + tl + (int64_t)kq * HID;
+  float av[AIT], bv[DF_K / 4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
+      const int mm = e / DF_K, kk = e % DF_K;
+      const bool ok = m0 + mm < count;
+      const float t = Ar[(int64_t)(ok ? m0 + mm : m0) * FEAT + k0 + kk];
+      av[i] = ok ? t : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < DF_K / 4; ++s) bv[s] = wl[(int64_t)(k0 + 4 * s) * HID];
+  };
+  load(0);
+  for (int k0 = 0; k0 < FEAT; k0 += DF_K) {
+    __syncthreads();  // previous chunk's readers done
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int e = tid + 256 * i;
+      a_s[(e / DF_K) * (DF_K + 1) + e % DF_K] = av[i];
+    }
+    float bc[DF_K / 4];
+#pragma unroll
+    for (int s = 0; s < DF_K / 4; ++s) bc[s] = bv[s];
+    load(min(k0 + DF_K, FEAT - DF_K));  // the last chunk re-loads itself (uniform, branch-free)
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < DF_K / 4; ++s) acc = mfma16(a_s[tl * (DF_K + 1) + 4 * s + kq], bc[s], acc);
+  }
+  const int col = n0 + tl;
+  const float bias = params[(int64_t)r * stride + OFF_B5 + col];
+  const uint64_t dkey = drop_key ? drop_key[r] : 0ull;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int row = m0 + 4 * kq + v;
+    if (row < count) {
+      const float z = acc[v] + bias;
+      const float h = fmaxf(z, 0.0f);
+      const int64_t o = ((int64_t)r * bmax + row) * HID + col;
+      if (drop_key) {
+        const bool keep = drop_keep(drop_row_seed(dkey, DROP_L5, (uint32_t)row), (uint32_t)col, THR_50);
+        H[o] = keep ? h * SCALE_50 : 0.0f;
+        code[o] = (uint8_t)((keep ? CODE_KEEP : 0) | (z > 0.0f ? CODE_POS : 0));
+      } else {
+        H[o] = h;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Head: Dense(10) + softmax-CE gradient (mean over the batch), dW6/db6 + RMSprop, dh5 through dropout'
 // and relu'.  One block per replica.
@@ -2356,8 +2438,12 @@ void enqueue_forward(hipStream_t s, int R, int B, const float* x, int in_mode, i
   CONV4_FWD<<<dim3(1, B, R), 256, 0, s>>>(c4);
   PE(4);
   PB(5);
-  dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, glob,
-                                                                      w5src, drop_key, h5, code5);
+  if (B <= MPLC_D5F16_MAX)
+    dense5_fwd16_kernel<<<dim3(1, HID / 64, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, glob, w5src,
+                                                             drop_key, h5, code5);
+  else
+    dense5_fwd_kernel<<<dim3((B + 31) / 32, HID / 128, R), 256, 0, s>>>(d4, cnt, cnt_all, B, params, stride, glob,
+                                                                        w5src, drop_key, h5, code5);
   PE(5);
 #undef PB
 #undef PE

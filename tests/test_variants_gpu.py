@@ -2,7 +2,9 @@
 
 build_native.build_variants() links mplc/lib/variants/libmplc_hip_alt.so with the MFMA form of MNIST's
 dense1_bwd_adam (MPLC_D1_MFMA=1; DESIGN.md 7e: bit-identical, +1.9 % at 5120 replicas so not the default) and
-the VALU form of CIFAR10's dense5_bwd (MPLC_D5_MFMA=0; bit-identical under the RMSprop no-contraction rule).
+the VALU form of CIFAR10's dense5_bwd (MPLC_D5_MFMA=0; bit-identical under the RMSprop no-contraction rule) and
+the 32-row form of its dense5_fwd at every batch size (MPLC_D5F16_MAX=0; the product runs the 16-row form up to 16
+samples per replica, exercised by the probe's small-batch CIFAR scenario).
 tests/variant_probe.py trains two epochs of small FedAvg / singleton coalitions of both models in a child process
 per library (MPLC_LIB_PATH); every final model row must hash the same."""
 import json
@@ -34,6 +36,6 @@ def test_alternate_dense_forms_bit_identical():
     var = _probe(alt)
     print(base, var)
     assert base["lib"] != var["lib"]
-    for model in ("mnist", "cifar10"):
+    for model in ("mnist", "cifar10", "cifar10_smallb"):
         assert var[model] == base[model], (model, base[model], var[model])
         assert max(base[model]["scores"]) > 0.35  # the models learned: the dense backward passes did real work

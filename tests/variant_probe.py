@@ -19,10 +19,14 @@ def main():
     from mplc.engine import CoalitionEngine
     from mplc.scenario import Scenario
     out = {"lib": os.path.relpath(_native.lib_path(), REPO)}
-    for name, maker in (("mnist", digits_as_mnist), ("cifar10", digits_as_cifar)):
+    # cifar10_smallb: batches of at most 16 samples (M=6, G=8: 6 / 9 / 15), the size at which dense5_fwd runs its
+    # 16-row form (the variant library runs the 32-row form there)
+    for name, maker, amounts, M, G in (("mnist", digits_as_mnist, [0.2, 0.5, 0.3], 2, 4),
+                                       ("cifar10", digits_as_cifar, [0.2, 0.5, 0.3], 2, 4),
+                                       ("cifar10_smallb", digits_as_cifar, [0.2, 0.3, 0.5], 6, 8)):
         x, y = maker()
-        ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:], **({"name": "cifar10"} if name == "cifar10" else {}))
-        sc = Scenario(3, [0.2, 0.5, 0.3], dataset=ds, minibatch_count=2, gradient_updates_per_pass_count=4,
+        ds = ArrayDataset(x[:1500], y[:1500], x[1500:], y[1500:], **({"name": "cifar10"} if "cifar" in name else {}))
+        sc = Scenario(3, amounts, dataset=ds, minibatch_count=M, gradient_updates_per_pass_count=G,
                       epoch_count=2, is_early_stopping=False).provision()
         eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=4 << 30, eval_budget_bytes=1 << 30)
         res = eng.evaluate([(0,), (1, 2), (0, 1, 2)], return_details=True, return_models=True)
