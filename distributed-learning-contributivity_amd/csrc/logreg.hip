@@ -36,7 +36,7 @@
 
 namespace {
 
-constexpr int LR_THREADS = 64;   // one wave per coalition
+constexpr int LR_THREADS = 64;   // one wave per fit (a fit kernel work item) / per coalition (averages)
 constexpr int LR_MAXF = 32;      // D = n_features + 1 unknowns (coef | intercept) supported
 constexpr int LR_MAXP = 64;      // partners per coalition
 constexpr int LR_NMAX = 64;      // rows staged in LDS at a time (config #2's fits: 56-57 rows; larger fits stream)
@@ -44,7 +44,7 @@ constexpr int LR_XS = LR_MAXF + 1;  // staged row stride in floats (odd: per-lan
 constexpr int LR_LS = LR_MAXF + 1;  // row stride of the Hessian / factor in LDS: lane li's row reads 2-way banked
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-// 19.3 KB: two one-wave workgroups per SIMD fit a CU's 160 KB of LDS
+// 18.5 KB: two one-wave workgroups per SIMD fit a CU's 160 KB of LDS
 struct Shared {
   double w[LR_MAXF];       // current Newton iterate (entries >= D stay 0)
   double trial[LR_MAXF];   // line-search trial point (entries >= D stay 0)
@@ -89,8 +89,8 @@ struct RowSel {
   }
 };
 
-// rows [c0, c0 + cn) of the fit into LDS as fp64 (exact widening of the fp32 data), the intercept's column of ones
-// and zero padding appended, labels as +-1
+// rows [c0, c0 + cn) of the fit into LDS as the data's fp32 (widened to fp64 exactly where read), the intercept's
+// column of ones and zero padding appended, labels as +-1
 __device__ void stage_rows(const RowSel& rs, int c0, int cn, const float* X, const float* Y, int F, Shared& sh) {
   const int lane = threadIdx.x;
   for (int i = lane; i < cn; i += LR_THREADS) {
