@@ -531,9 +531,11 @@ def bench_train(args, rank, world):
     # and the config #4 sub-leg (one CIFAR10 TMCS run: ~110 s on one GPU)
     # (measured on the box, round 3: aggregation 1.3 s, CPU baselines 13 s + 6 s, the CIFAR run 107 s)
     # and the config #2 sub-leg (Titanic: a warm-up and a few sub-second sweeps, its CPU baseline 10 s)
+    # and the reference-tutorial sub-leg (engine set-up, a warm-up and three 1.7 s sweeps)
     reserve = ((0 if args.no_shapley_agg else 10) + (25 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
                + (0 if args.no_cifar else CIFAR_SUBLEG_S / world + 15 + (15 if world == 1 else 0))
-               + (0 if args.no_titanic else 15 + (12 if world == 1 and not args.no_cpu_baseline else 0)))
+               + (0 if args.no_titanic else 15 + (12 if world == 1 and not args.no_cpu_baseline else 0))
+               + (0 if args.no_tutorial else 20))
     steps, warm, wall, c, per_step = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
@@ -945,6 +947,56 @@ def bench_titanic(args, rank, world, sub=False):
     return out, sc, coals
 
 
+# The reference's own published timing of this path: notebooks/tutorials/
+# Tutorial-2_Add_contributivity_measurement.ipynb, exact "Shapley values" on MNIST, 3 partners [0.001, 0.699, 0.3],
+# E=10, M=3 (7 coalitions): "Computation time" 1525.8 s on a Colab GPU (model not printed), real MNIST
+REFERENCE_TUTORIAL_S, REFERENCE_TUTORIAL_COALITIONS = 1525.8, 7
+
+
+def bench_tutorial(args, rank, world, sub=False):
+    """The reference tutorial's exact-Shapley experiment (the only published timing of this path):
+    MNIST-shaped synthetic data at the full MNIST sizes (54,000 train / 6,000 val / 10,000 test rows), 3 partners
+    [0.001, 0.699, 0.3], E=10, M=3, G=8 (the reference defaults; early stopping cannot act within 10 epochs at patience
+    10), "Shapley values" over the 7 coalitions.  vs_baseline = this line's evals/s over the tutorial's 7 / 1525.8 s."""
+    import torch
+    from mplc.contributivity import Contributivity
+    from mplc.dataset import Mnist
+    from mplc.engine import CoalitionEngine
+    from mplc.scenario import Scenario
+    sc = Scenario(3, [0.001, 0.699, 0.3], dataset=Mnist(synthetic=True, signal=0.2), epoch_count=10,
+                  minibatch_count=3).provision()
+    sc.engine = CoalitionEngine.for_scenario(sc)
+
+    def one_step():
+        sc.coalition_values = {}
+        c = Contributivity(scenario=sc)
+        c.compute_contributivity("Shapley values")
+        torch.cuda.synchronize()
+        return c
+
+    steps, warm, wall, c, per_step = run_budgeted(one_step, lambda i, n: one_step(), args, world, 0, "tutorial",
+                                                  max_steps=3 if sub else None, warmup=1)
+    value = c.first_charac_fct_calls_count * steps / wall
+    ref = REFERENCE_TUTORIAL_COALITIONS / REFERENCE_TUTORIAL_S
+    out = {"metric": "coalition v(S) evals/sec (reference Tutorial-2: MNIST exact Shapley, 3 partners, E=10, M=3)",
+           "value": round(value, 4), "unit": "coalition evals/s", "n_gpus": world, "steps": steps, "warmup": warm,
+           "ms_per_step": round(wall * 1000 / steps, 1), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": round(value / ref, 1), "dtype": "f32",
+           "data": "synthetic (MNIST-shaped, learnable: class templates at signal 0.2, the full MNIST sizes; the "
+                   "tutorial ran real MNIST)",
+           "config": {"workload": "reference Tutorial-2 (notebooks/tutorials/Tutorial-2_Add_contributivity_measurement"
+                                  ".ipynb): MNIST CNN, 3 partners [0.001, 0.699, 0.3], FedAvg, E=10, M=3, G=8, exact "
+                                  f"Shapley over the 7 coalitions, coalitions LPT-sharded x{world}",
+                      "batch_size": [p.batch_size for p in sc.partners_list],
+                      "coalitions_evaluated": c.first_charac_fct_calls_count,
+                      "shapley": [round(float(v), 6) for v in c.contributivity_scores],
+                      "per_step_ms": [round(t * 1000, 1) for t in per_step],
+                      "baseline": {"value": round(ref, 5), "unit": "coalition evals/s",
+                                   "source": "the tutorial notebook's printed computation time, 1525.8 s for 7 "
+                                             "coalitions on a Colab GPU (BASELINE.md section 1)"}}}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -952,7 +1004,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--budget-s", type=float, default=480.0,
                     help="wall-clock budget from process start for the whole run (driver limit: 600 s)")
-    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar", "titanic", "dist-check"])
+    ap.add_argument("--leg", default="train", choices=["train", "shapley", "cifar", "titanic", "tutorial", "dist-check"])
     ap.add_argument("--method", default="TMCS")
     ap.add_argument("--signal", type=float, default=0.4)
     ap.add_argument("--cifar-epochs", type=int, default=1)
@@ -967,6 +1019,8 @@ def main():
     ap.add_argument("--no-shapley-agg", action="store_true")
     ap.add_argument("--no-cifar", action="store_true", help="leave out the config #4 sub-leg of the default line")
     ap.add_argument("--no-titanic", action="store_true", help="leave out the config #2 sub-leg of the default line")
+    ap.add_argument("--no-tutorial", action="store_true",
+                    help="leave out the reference-tutorial sub-leg (vs its published timing) of the default line")
     ap.add_argument("--early-stopping", action="store_true",
                     help="train leg at the reference's stopping rule (with --epochs 40: its defaults)")
     ap.add_argument("--mnist-signal", type=float, default=0.0,
@@ -1016,6 +1070,9 @@ def main():
                                                                 f"range-sharded + RCCL all-reduce x{world}"}})
         if rank == 0:
             out["cpu_baseline"] = cpu_baseline_shapley() if (world == 1 and not args.no_cpu_baseline) else None
+    elif args.leg == "tutorial":
+        out = bench_tutorial(args, rank, world)
+        out["cpu_baseline"] = None
     elif args.leg == "titanic":
         out, sc, coals = bench_titanic(args, rank, world)
         if rank == 0:
@@ -1065,6 +1122,14 @@ def main():
                 c2.pop(k, None)
             out["config2"] = c2
             log(f"config #2 sub-leg: {c2['value']} evals/s")
+        if not args.no_tutorial:
+            # the reference's only published timing of this path (its Tutorial-2 exact-Shapley run), with
+            # vs_baseline against it: a few seconds
+            tut = bench_tutorial(args, rank, world, sub=True)
+            for k in ("n_gpus", "higher_is_better", "scaling", "budget"):
+                tut.pop(k, None)
+            out["tutorial"] = tut
+            log(f"tutorial sub-leg: {tut['value']} evals/s, {tut['vs_baseline']}x the reference's published run")
         if rank == 0:
             out["cpu_baseline"] = (cpu_baseline_train(sc, args.epochs, args.minibatches)
                                    if (world == 1 and not args.no_cpu_baseline) else None)
