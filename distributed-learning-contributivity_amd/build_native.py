@@ -104,11 +104,13 @@ def build(verbose=False, force=False, jobs=8, sanitize=False):
 
 # Alternate kernel forms kept in the source because they are bit-identical to the product kernels (the matrix core
 # accumulates as an fma chain) and win at other batch sizes: the MFMA form of MNIST's dense1_bwd_adam
-# (MPLC_D1_MFMA=1), the VALU form of CIFAR's dense5_bwd (MPLC_D5_MFMA=0) and the 32-row form of its dense5_fwd at
-# every batch size (MPLC_D5F16_MAX=0).  build() links them into one variant
+# (MPLC_D1_MFMA=1), the VALU form of CIFAR's dense5_bwd (MPLC_D5_MFMA=0), the 32-row form of its dense5_fwd at
+# every batch size (MPLC_D5F16_MAX=0) and conv4_fwd's remainder group as a padded 16-tile MFMA group instead of
+# 4x4x1 MFMAs (MPLC_WINO_QUAD=0).  build() links them into one variant
 # library, mplc/lib/variants/libmplc_hip_alt.so, which tests/test_variants_gpu.py runs against the product library
 # (bit-identical models), so the non-default bodies cannot rot unseen.
-VARIANTS = {"alt": {"mnist_cnn.hip": ["-DMPLC_D1_MFMA=1"], "cifar_cnn.hip": ["-DMPLC_D5_MFMA=0", "-DMPLC_D5F16_MAX=0"]}}
+VARIANTS = {"alt": {"mnist_cnn.hip": ["-DMPLC_D1_MFMA=1"], "cifar_cnn.hip": ["-DMPLC_D5_MFMA=0", "-DMPLC_D5F16_MAX=0",
+                                                                         "-DMPLC_WINO_QUAD=0"]}}
 VARIANT_DIR = os.path.join(LIB_DIR, "variants")
 
 

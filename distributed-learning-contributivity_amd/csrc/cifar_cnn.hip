@@ -86,6 +86,13 @@ __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_4x4x1f32: 16 blocks of 4x4, K = 1.  Block b takes A[b][i] from lane 4b + i and B[b][j] from lane
+// 4b + j; D[b][i][j] lands in lane 4b + j, register i.  Each output is fmaf(a, b, c) (measured on 2^20 outputs,
+// scripts/probes/mfma_4x4.hip), issued in 8-10 cycles per SIMD: the rate of the 16x16x4 form at a quarter of its M.
+__device__ __forceinline__ fvec4 mfma4(float a, float b, fvec4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ floatx16 zero16() {
   floatx16 z;
 #pragma unroll
@@ -649,6 +656,11 @@ __global__ __launch_bounds__(256) void wino_u_kernel(const float* __restrict__ p
   }
 }
 
+#ifndef MPLC_WINO_QUAD
+#define MPLC_WINO_QUAD 1  // conv4_fwd's 4-tile remainder group on 4x4x1 MFMAs (0: a padded 16-tile group; same bits)
+#endif
+
+
 // Wave-index tag: a loop instantiated once per wave index (compile-time Winograd transform signs)
 template <int V>
 struct IntC {
@@ -672,6 +684,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int TQ = 16 * TS;
   constexpr int NK = CI / 4;
   static_assert(CI % 4 == 0 && CO % 32 == 0, "channel counts");
+  // one band whose last 16-tile group holds exactly 4 tiles, 64 output channels: that group on 4x4x1 MFMAs
+  constexpr bool QUAD = MPLC_WINO_QUAD && BTY >= TYT && (BTY * TXT) % 16 == 4 && CO == 64;
   static_assert((16 * CH) % 256 == 0, "output items per thread");
   // the data gradients' epilogue operand (EPI_BWD_MASK: the ReLU' mask a > 0; EPI_BWD_UNPOOL: the pool codes) for
   // the band's 2 BTY output rows, staged as bytes with the input band: its global loads share the staging's latency
@@ -802,13 +816,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int ra = (WIC == 0) ? 0 : 1;
   constexpr int rb = (WIC == 3) ? 3 : 2;
   const int drow = (rb - ra) * ROWP;
+  // The QUAD group's GEMMs (4 tiles x 64 channels per transform point, K = CI) on 4x4x1 MFMAs: lane 4 b + i
+  // supplies tile i's V (the same value in all 16 blocks), lane = output channel supplies U; the wave's 4 transform
+  // points are 4 accumulators.  U streams from L2 in chunks of QC channels, the next chunk in flight.
+  auto quad_group = [&](int t0, fvec4 (&q)[4]) __attribute__((always_inline)) {
+    const int tile = t0 + (lane & 3);
+    const int tyl = tile / TXT, tx = tile % TXT;
+    const float* dpa = in_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP;
+    const float* Uq = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + (lane & (CO - 1));
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) q[jj] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int QC = 8;  // 16: 208 registers spilled
+    constexpr int NCH = CI / QC;
+    static_assert(CI % (2 * QC) == 0, "channel chunks in pairs");
+    auto qload = [&](int ch, float (&b)[QC][4]) {
+#pragma unroll
+      for (int u = 0; u < QC; ++u)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) b[u][jj] = Uq[(int64_t)jj * CI * CO + (ch * QC + u) * CO];
+    };
+    auto qstep = [&](int ch, const float (&b)[QC][4]) {
+#pragma unroll
+      for (int u = 0; u < QC; ++u) {
+        const float* d0 = dpa + ch * QC + u;
+        float t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float da = d0[c * CIP], db = d0[drow + c * CIP];
+          t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+        }
+        float v[4];
+        v[0] = t[0] - t[2];
+        v[1] = t[1] + t[2];
+        v[2] = t[2] - t[1];
+        v[3] = t[1] - t[3];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) q[jj] = mfma4(v[jj], b[u][jj], q[jj]);
+      }
+    };
+    float qb0[QC][4], qb1[QC][4];
+    qload(0, qb0);
 #pragma unroll 1
-  for (int g = 0; g < NG; ++g) {
-    if (16 * g >= ntile) break;  // block-uniform
+    for (int ch = 0; ch < NCH; ch += 2) {
+      qload(ch + 1, qb1);
+      qstep(ch, qb0);
+      if (ch + 2 < NCH) qload(ch + 2, qb0);
+      qstep(ch + 1, qb1);
+    }
+  };
+  // QUAD: the band's last group holds 4 tiles (conv4's 6 x 6 windows: 36 = 2 x 16 + 4).  Instead of a 16-row
+  // MFMA group three quarters padding, its GEMMs run on v_mfma_f32_4x4x1f32 with the 4 tiles as rows and the 64
+  // output channels as 16 blocks of 4 columns: a quarter of the matrix-core cycles.  Per output the products
+  // chain over ci = 0, 1, .. 63 from zero exactly as the 16x16x4 form's k-steps do (fmaf per element in ci
+  // order): the same bits.  The output transform below is shared.  The group runs after the loop, where the
+  // register copy of U (bw) is dead.
+  auto run_group = [&](int g, auto qtag) __attribute__((always_inline)) {
+    constexpr bool quad = decltype(qtag)::value != 0;
+    fvec4 acc4[4];
+    fvec4 acc[4][NCG];
+    if constexpr (quad) {
+      quad_group(16 * g, acc4);
+    } else {
     const int tile = min(16 * g + tl, ntile - 1);
     const int tyl = tile / TXT, tx = tile % TXT;
     const float* dpa = in_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP + kq;
-    fvec4 acc[4][NCG];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
@@ -846,8 +917,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         kstep(st + 1, b1);
       }
     }
+    }  // 16-tile group
 #pragma unroll
     for (int pass = 0; pass < NPASS; ++pass) {
+      if constexpr (quad) {
+        // lane = output channel; register i = tile i of the group
+        if ((lane >> 5) == pass) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float m0 = acc4[0][i], m1 = acc4[1][i], m2 = acc4[2][i], m3 = acc4[3][i];
+            const int off = i * TS + (lane & 31);
+            t_s[(2 * wi) * TQ + off] = (m0 + m1) + m2;
+            t_s[(2 * wi + 1) * TQ + off] = (m1 - m2) - m3;
+          }
+        }
+      } else {
       // T_i[b] = sum_j M_ij A[j][b]: lane holds tiles 4 kq + rr of the group, channel 16 cg + tl
 #pragma unroll
       for (int cgl = 0; cgl < CH / 16; ++cgl)
@@ -859,6 +943,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           t_s[(2 * wi) * TQ + off] = (m0 + m1) + m2;
           t_s[(2 * wi + 1) * TQ + off] = (m1 - m2) - m3;
         }
+      }
       __syncthreads();
       // Y[a][b] = sum_i A^T[a][i] T_i[b]: Y0b = T0b + T1b + T2b, Y1b = T1b - T2b - T3b; tile pixel q = 2a + b
 #pragma unroll
@@ -924,7 +1009,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
       __syncthreads();
     }
+  };
+#pragma unroll 1
+  for (int g = 0; g < NG - (QUAD ? 1 : 0); ++g) {
+    if (16 * g >= ntile) break;  // block-uniform
+    run_group(g, IntC<0>{});
   }
+  if constexpr (QUAD) run_group(NG - 1, IntC<1>{});
   };
   switch (wi) {  // wave-uniform
     case 0: groups(IntC<0>{}); break;

@@ -4,7 +4,8 @@ build_native.build_variants() links mplc/lib/variants/libmplc_hip_alt.so with th
 dense1_bwd_adam (MPLC_D1_MFMA=1; DESIGN.md 7e: bit-identical, +1.9 % at 5120 replicas so not the default) and
 the VALU form of CIFAR10's dense5_bwd (MPLC_D5_MFMA=0; bit-identical under the RMSprop no-contraction rule) and
 the 32-row form of its dense5_fwd at every batch size (MPLC_D5F16_MAX=0; the product runs the 16-row form up to 16
-samples per replica, exercised by the probe's small-batch CIFAR scenario).
+samples per replica, exercised by the probe's small-batch CIFAR scenario) and conv4_fwd's 4-tile remainder group as a
+padded 16-tile group (MPLC_WINO_QUAD=0; the product runs it on v_mfma_f32_4x4x1f32).
 tests/variant_probe.py trains two epochs of small FedAvg / singleton coalitions of both models in a child process
 per library (MPLC_LIB_PATH); every final model row must hash the same."""
 import json
