@@ -40,8 +40,11 @@ def _stale(target, deps):
 # Per-source extra flags.  mnist_cnn.hip: no SLP vectorisation - packed f32 VALU (v_pk_add_f32 and the v_mov
 # shuffles that feed it) issued beside f32 MFMAs costs more issue cycles than the scalar ops it replaces
 # (MI355X_MICROARCH.md, per-instruction cycle constants), and it hoisted the Winograd V arithmetic of the
-# software-pipelined conv k-loops out of the MFMA gaps.
-FILE_FLAGS = {"mnist_cnn.hip": ["-fno-slp-vectorize"], "mnist_wgrad.hip": ["-fno-slp-vectorize"]}
+# software-pipelined conv k-loops out of the MFMA gaps.  cifar_cnn.hip likewise (its Winograd loops: 10-25 % fewer
+# VALU instructions; every VALU instruction costs an f32 MFMA stream 2.5-3.5 cycles); its two head
+# kernels live in cifar_head.hip with the default flags, which keeps their expf / logf / dot-product code as it was.
+FILE_FLAGS = {"mnist_cnn.hip": ["-fno-slp-vectorize"], "mnist_wgrad.hip": ["-fno-slp-vectorize"],
+              "cifar_cnn.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src, obj, verbose):

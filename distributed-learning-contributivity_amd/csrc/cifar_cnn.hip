@@ -25,115 +25,9 @@
 #include "xcd.h"
 #include "mplc_hip.h"
 #include "mplc_hip_cifar.h"
+#include "cifar_common.h"
 
 namespace {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float fvec4 __attribute__((ext_vector_type(4)));
-
-constexpr int64_t OFF_W1 = MPLC_CIFAR_OFF_W1, OFF_B1 = MPLC_CIFAR_OFF_B1, OFF_W2 = MPLC_CIFAR_OFF_W2,
-                  OFF_B2 = MPLC_CIFAR_OFF_B2, OFF_W3 = MPLC_CIFAR_OFF_W3, OFF_B3 = MPLC_CIFAR_OFF_B3,
-                  OFF_W4 = MPLC_CIFAR_OFF_W4, OFF_B4 = MPLC_CIFAR_OFF_B4, OFF_W5 = MPLC_CIFAR_OFF_W5,
-                  OFF_B5 = MPLC_CIFAR_OFF_B5, OFF_W6 = MPLC_CIFAR_OFF_W6, OFF_B6 = MPLC_CIFAR_OFF_B6;
-constexpr int64_t STRIDE = MPLC_CIFAR_STRIDE;
-constexpr int IMG_SZ = 32 * 32 * 3;
-constexpr int FEAT = MPLC_CIFAR_D4;  // 2304
-constexpr int HID = MPLC_CIFAR_H5;   // 512
-constexpr int NCLS = 10;
-constexpr int WGS = MPLC_CIFAR_WG_SAMPLES;
-constexpr int WPART = MPLC_CIFAR_WPART;
-
-// dropout (Keras Dropout -> tf.nn.dropout: (x * (1/(1-rate))) * (u >= rate)); u = 24-bit keyed counter
-constexpr uint32_t DROP_L2 = 2, DROP_L4 = 4, DROP_L5 = 5;
-constexpr uint32_t THR_25 = 1u << 22;  // 0.25 * 2^24
-constexpr uint32_t THR_50 = 1u << 23;  // 0.5 * 2^24
-constexpr float SCALE_25 = 0x1.555556p+0f;  // float(1 / 0.75)
-constexpr float SCALE_50 = 2.0f;
-constexpr uint8_t CODE_KEEP = 0x40, CODE_POS = 0x80;
-
-// 32-bit finaliser (lowbias32): a bijection with full avalanche; 2 multiplies, cheap next to the 64-bit mix.
-__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-// keep(element e) = top 24 bits of hash32(row_seed ^ e) >= rate * 2^24, row_seed = drop_row_seed(step key,
-// layer, slot j): one hash per element (restated in oracle/cifar_cnn.py).
-__device__ __forceinline__ uint32_t drop_row_seed(uint64_t dkey, uint32_t layer, uint32_t j) {
-  return hash32((uint32_t)dkey ^ hash32((uint32_t)(dkey >> 32) ^ (layer << 24) ^ j));
-}
-
-__device__ __forceinline__ bool drop_keep(uint32_t row_seed, uint32_t e, uint32_t thr) {
-  return (hash32(row_seed ^ e) >> 8) >= thr;
-}
-
-// Cross-lane add within rows of 16 lanes on DPP (VALU, no LDS round trip).  Each level adds the partner's
-// value exactly as `d += __shfl_xor(d, m)` does (commutative adds of the same operands: bit-identical).
-template <int CTRL>
-__device__ __forceinline__ float dpp_partner(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
-constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
-constexpr int DPP_HALF_MIRROR = 0x141;  // lane i <-> 7 - i within 8 (the other quad after two levels)
-constexpr int DPP_MIRROR = 0x140;       // lane i <-> 15 - i within 16 (the other 8 after three levels)
-
-__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-// v_mfma_f32_4x4x1f32: 16 blocks of 4x4, K = 1.  Block b takes A[b][i] from lane 4b + i and B[b][j] from lane
-// 4b + j; D[b][i][j] lands in lane 4b + j, register i.  Each output is fmaf(a, b, c) (measured on 2^20 outputs,
-// scripts/probes/mfma_4x4.hip), issued in 8-10 cycles per SIMD: the rate of the 16x16x4 form at a quarter of its M.
-__device__ __forceinline__ fvec4 mfma4(float a, float b, fvec4 c) {
-  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ floatx16 zero16() {
-  floatx16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.0f;
-  return z;
-}
-
-// accumulator register -> row within a 32-row tile (v_mfma_f32_32x32x2f32 C/D layout)
-__device__ __forceinline__ int acc_row(int reg, int kh) { return (reg & 3) + 8 * (reg >> 2) + 4 * kh; }
-
-// ------------------------------------------------------------------------------------------------
-// Keras 2.3.1 RMSprop (keras/optimizers.py): lr_t = lr / (1 + decay * iterations) with the iteration
-// count before this update; a = rho a + (1 - rho) g^2; p -= lr_t g / (sqrt(a) + eps).  (1 - rho) comes
-// from the host (a Python double rounded once to fp32, as Keras does).  A fresh optimizer (FedAvg partner
-// fit, t == 1) has a == 0.
-// ------------------------------------------------------------------------------------------------
-struct RmsCfg {
-  float lr_t, rho, one_m_rho, eps;
-  bool reset;
-};
-
-__device__ __forceinline__ RmsCfg rms_cfg(int t, float lr, float rho, float omr, float decay, float eps) {
-  RmsCfg c;
-  const float it = (float)(t - 1);
-  c.lr_t = lr * (1.0f / (1.0f + decay * it));
-  c.rho = rho;
-  c.one_m_rho = omr;
-  c.eps = eps;
-  c.reset = (t == 1);
-  return c;
-}
-
-__device__ __forceinline__ void rms_apply(float& p, float& a, float g, const RmsCfg& c) {
-  // Keras evaluates rho a + (1 - rho) g^2 as separate multiplies and an add: no fused multiply-add here, in every
-  // kernel (the compiler's contraction otherwise depends on how it vectorised the caller)
-#pragma clang fp contract(off)
-  const float a0 = c.reset ? 0.0f : a;
-  const float an = c.rho * a0 + c.one_m_rho * (g * g);
-  p = p - c.lr_t * g / (sqrtf(an) + c.eps);
-  a = an;
-}
 
 // ------------------------------------------------------------------------------------------------
 // init (glorot_uniform from mix64(key + i*golden), as mplc_cnn_init_params), schedule, flipped weights
@@ -1912,126 +1806,6 @@ __global__ __launch_bounds__(256) void dense5_fwd16_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Head: Dense(10) + softmax-CE gradient (mean over the batch), dW6/db6 + RMSprop, dh5 through dropout'
-// and relu'.  One block per replica.
-// ------------------------------------------------------------------------------------------------
-constexpr int HEAD_CHUNK = 256;
-constexpr int W6N = HID * NCLS + NCLS;  // W6 and b6 are contiguous
-constexpr int HEAD_G = (W6N + 255) / 256;
-
-__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ D5, const uint8_t* __restrict__ code5,
-                                                   const int32_t* __restrict__ idx, const int32_t* __restrict__ labels,
-                                                   const int32_t* __restrict__ cnt, const int32_t* __restrict__ opt_t,
-                                                   int bmax, float* __restrict__ params, float* __restrict__ rms,
-                                                   float* __restrict__ dH, float lr, float rho, float omr,
-                                                   float decay, float eps, double* __restrict__ hstats) {
-  __shared__ float w6_s[W6N];
-  __shared__ float dl_s[HEAD_CHUNK * NCLS];
-  __shared__ double hs_s[2][HEAD_CHUNK];
-  const int r = blockIdx.x;
-  const int count = cnt[r];
-  const int tid = threadIdx.x;
-  if (count == 0) {
-    if (hstats && tid < 3) hstats[(int64_t)r * 3 + tid] = 0.0;
-    return;
-  }
-  float* P = params + (int64_t)r * STRIDE;
-  for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
-  __syncthreads();
-  const float inv_b = 1.0f / (float)count;
-  float gacc[HEAD_G];
-#pragma unroll
-  for (int u = 0; u < HEAD_G; ++u) gacc[u] = 0.0f;
-  double hl = 0.0, hc = 0.0;  // this thread's training CE / correct sums (hstats)
-  const float* Dr = D5 + (int64_t)r * bmax * HID;
-  for (int c0 = 0; c0 < count; c0 += HEAD_CHUNK) {
-    const int cn = min(HEAD_CHUNK, count - c0);
-    if (tid < cn) {
-      const int jj = c0 + tid;
-      const float* h = Dr + (int64_t)jj * HID;
-      float z[NCLS];
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
-      for (int c = 0; c < HID; ++c) {
-        const float hv = h[c];
-#pragma unroll
-        for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
-      }
-      const int y = labels[idx[(int64_t)r * bmax + jj]];
-      int am = 0;  // first maximum (the evaluation's argmax)
-      float mx = z[0];
-#pragma unroll
-      for (int o = 1; o < NCLS; ++o)
-        if (z[o] > mx) { mx = z[o]; am = o; }
-      float zy = z[0];
-#pragma unroll
-      for (int o = 1; o < NCLS; ++o) zy = (o == y) ? z[o] : zy;
-      float s = 0.0f;
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) { z[o] = expf(z[o] - mx); s += z[o]; }
-      hl += (double)(logf(s) + mx - zy);
-      hc += (am == y) ? 1.0 : 0.0;
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) dl_s[tid * NCLS + o] = (z[o] / s - (o == y ? 1.0f : 0.0f)) * inv_b;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < HEAD_G; ++u) {
-      const int e = tid + 256 * u;
-      if (e < HID * NCLS) {
-        const int c = e / NCLS, o = e % NCLS;
-        float acc = 0.0f;
-        for (int jj = 0; jj < cn; ++jj) acc += Dr[(int64_t)(c0 + jj) * HID + c] * dl_s[jj * NCLS + o];
-        gacc[u] += acc;
-      } else if (e < W6N) {
-        const int o = e - HID * NCLS;
-        float acc = 0.0f;
-        for (int jj = 0; jj < cn; ++jj) acc += dl_s[jj * NCLS + o];
-        gacc[u] += acc;
-      }
-    }
-    const uint8_t* cd = code5 + (int64_t)r * bmax * HID;
-    for (int e = tid; e < cn * HID; e += 256) {
-      const int jj = e / HID, c = e % HID;
-      float acc = 0.0f;
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) acc += dl_s[jj * NCLS + o] * w6_s[c * NCLS + o];
-      const uint32_t k = cd[(int64_t)(c0 + jj) * HID + c];
-      dH[((int64_t)r * bmax + c0 + jj) * HID + c] =
-          ((k & CODE_KEEP) && (k & CODE_POS)) ? acc * SCALE_50 : 0.0f;
-    }
-    __syncthreads();
-  }
-  if (hstats) {  // the step's training loss / accuracy sums before the update (Keras fit history)
-    hs_s[0][tid] = hl;
-    hs_s[1][tid] = hc;
-    __syncthreads();
-    for (int off = HEAD_CHUNK / 2; off >= 1; off >>= 1) {
-      if (tid < off) { hs_s[0][tid] += hs_s[0][tid + off]; hs_s[1][tid] += hs_s[1][tid + off]; }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      hstats[(int64_t)r * 3] = hs_s[0][0];
-      hstats[(int64_t)r * 3 + 1] = hs_s[1][0];
-      hstats[(int64_t)r * 3 + 2] = (double)count;
-    }
-  }
-  const RmsCfg cfg = rms_cfg(opt_t[r], lr, rho, omr, decay, eps);
-  float* Rr = rms + (int64_t)r * STRIDE;
-#pragma unroll
-  for (int u = 0; u < HEAD_G; ++u) {
-    const int e = tid + 256 * u;
-    if (e < W6N) {
-      const int64_t o = OFF_W6 + e;
-      float p = P[o], aa = Rr[o];
-      rms_apply(p, aa, gacc[u], cfg);
-      P[o] = p;
-      Rr[o] = aa;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // Dense(512) backward + RMSprop, per 32-row slice of W5, 8 rows at a time (32 threads per row, 4 fvec4
 // each: every access instruction covers 512 contiguous bytes of a row); dh5 is staged in LDS once per
 // block for its 4 row groups:
@@ -2361,72 +2135,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ------------------------------------------------------------------------------------------------
-// Evaluation head: logits, accuracy count and summed cross-entropy per model (deterministic order).
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void eval_head_kernel(const float* __restrict__ H, int count, int chunk,
-                                                        const int32_t* __restrict__ labels, int row_base,
-                                                        const float* __restrict__ params, int64_t stride,
-                                                        int32_t* __restrict__ correct, double* __restrict__ loss_sum) {
-  __shared__ float w6_s[W6N];
-  __shared__ double ls[256];
-  __shared__ int cs[256];
-  const int mdl = blockIdx.x;
-  const int tid = threadIdx.x;
-  const float* P = params + (int64_t)mdl * stride;
-  for (int e = tid; e < W6N; e += 256) w6_s[e] = P[OFF_W6 + e];
-  __syncthreads();
-  // The loss is summed in fixed blocks of 256 samples (the tree below), added to the model's running total in
-  // block order: with every chunk but the last a multiple of 256 samples (the host's rule), the total is the same
-  // bits whatever the chunk size - and the chunk size depends on how many models share the evaluation.
-  double run = (tid == 0) ? loss_sum[mdl] : 0.0;
-  int csum = 0;
-  for (int b0 = 0; b0 < count; b0 += 256) {
-    const int jj = b0 + tid;
-    double lv = 0.0;
-    if (jj < count) {
-      const float* h = H + ((int64_t)mdl * chunk + jj) * HID;
-      float z[NCLS];
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) z[o] = w6_s[HID * NCLS + o];
-      for (int c = 0; c < HID; ++c) {
-        const float hv = h[c];
-#pragma unroll
-        for (int o = 0; o < NCLS; ++o) z[o] += hv * w6_s[c * NCLS + o];
-      }
-      int am = 0;
-      float mx = z[0];
-#pragma unroll
-      for (int o = 1; o < NCLS; ++o)
-        if (z[o] > mx) { mx = z[o]; am = o; }
-      float s = 0.0f;
-#pragma unroll
-      for (int o = 0; o < NCLS; ++o) s += expf(z[o] - mx);
-      const int y = labels[row_base + jj];
-      lv = (double)(logf(s) + mx - z[y]);
-      csum += (am == y) ? 1 : 0;
-    }
-    ls[tid] = lv;
-    __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-      if (tid < off) ls[tid] += ls[tid + off];
-      __syncthreads();
-    }
-    if (tid == 0) run += ls[0];
-    __syncthreads();  // ls is rewritten by the next block
-  }
-  cs[tid] = csum;
-  __syncthreads();
-  for (int off = 128; off >= 1; off >>= 1) {
-    if (tid < off) cs[tid] += cs[tid + off];
-    __syncthreads();
-  }
-  if (tid == 0) {
-    correct[mdl] += cs[0];
-    loss_sum[mdl] = run;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // layer instantiations: <HI, WI, CI, CO, PAD, BR, NW, UM, EPI> (conv) and <HI, WI, CI, CO, PAD, HOV, WOV,
 // BR, NW> (wgrad); geometry checked by static_asserts, LDS per block in the comment
 // ------------------------------------------------------------------------------------------------
@@ -2599,8 +2307,8 @@ int mplc_cifar_train_step(const mplc_cifar_train_t* t, void* stream) {
                   t->a3, t->d4, t->code4, t->d5, t->code5, t->prof_kernel, t->prof_begin, t->prof_end, t->wt,
                   t->glob, w5src);
   PROF_BEGIN(6);
-  head_kernel<<<R, 256, 0, s>>>(t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5,
-                                t->lr, t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
+  cifar_launch_head(R, s, t->d5, t->code5, t->idx, t->labels, t->cnt, t->opt_t, B, t->params, t->rms, t->dh5, t->lr,
+                    t->rho, t->one_minus_rho, t->decay, t->eps, t->hstats);
   PROF_END(6);
   PROF_BEGIN(7);
 #if MPLC_D5_MFMA
@@ -2683,7 +2391,7 @@ int mplc_cifar_evaluate(const float* params, int64_t stride, int n_models, const
     const int cn = n_samples - s0 < chunk ? n_samples - s0 : chunk;
     enqueue_forward(s, n_models, chunk, x, 2, s0, nullptr, nullptr, cn, params, stride, nullptr, a1, d2, nullptr, a3,
                     d4, nullptr, h5, nullptr, 0, nullptr, nullptr, wu, nullptr, nullptr, false);
-    eval_head_kernel<<<n_models, 256, 0, s>>>(h5, cn, chunk, labels, s0, params, stride, correct, loss_sum);
+    cifar_launch_eval_head(n_models, s, h5, cn, chunk, labels, s0, params, stride, correct, loss_sum);
     const int st = launch_status();
     if (st) return st;
   }
