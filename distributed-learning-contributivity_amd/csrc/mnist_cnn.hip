@@ -193,12 +193,13 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
   // ---- Winograd GEMM roles: wave = transform row i; lane (tl = lane & 15, kq = lane >> 4)
   const int wi = wave;
   const int tl = lane & 15, kq = lane >> 4;
-  // B^T row i combines input rows (ra, rb) with signs (sa, sb): t = sa*d[ra] + sb*d[rb]
-  const int ra = (wi == 0) ? 0 : 1;
-  const int rb = (wi == 3) ? 3 : 2;
-  const float sa = (wi == 2) ? -1.0f : 1.0f;
-  const float sb = (wi == 0 || wi == 3) ? -1.0f : 1.0f;
-  const int drow = (rb - ra) * A1 * A1P;
+  // B^T row i combines two input rows: t = d[ry] + sx d[rx] (row 0: d0 - d2, 1: d1 + d2, 2: d2 - d1, 3: d1 - d3),
+  // one fused multiply-add by +-1 per value: the product is exact, so it rounds once, as the add or subtract does
+  // (a VALU instruction costs an f32 MFMA stream 2.5-3.5 cycles, DESIGN.md 7f: this was a multiply and an fma)
+  const int ry = (wi == 0) ? 0 : (wi == 2) ? 2 : 1;
+  const int rx = (wi == 3) ? 3 : (wi == 2) ? 1 : 2;
+  const float sx = (wi == 1) ? 1.0f : -1.0f;
+  const int drow = (rx - ry) * A1 * A1P;
   // the wave's B operands of all 8 k-steps (its transform row of U), resident for the whole block
   const float* Ub = U + (int64_t)r * MPLC_CNN_W2T + (int64_t)(4 * wi) * C1 * C2 + kq * C2 + tl;
   const float bias = P[OFF_B2 + (tid & 63)];  // the output phase's channel co = tid & 63 in every pass
@@ -247,8 +248,8 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll 1
     for (int g = 0; g < 3; ++g) {  // one 16-tile group at a time
       const int tile = 16 * g + tl;
-      // this lane's patch origin (row 2ty + ra, col 2tx) in a1_s, + channel kq
-      const int pa = ((2 * (tile / PL) + ra) * A1 + 2 * (tile % PL)) * A1P + kq;
+      // this lane's patch origin (row 2ty + ry, col 2tx) in a1_s, + channel kq
+      const int pa = ((2 * (tile / PL) + ry) * A1 + 2 * (tile % PL)) * A1P + kq;
       fvec4 acc[4][4];  // [j][channel group]
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
       auto make_v = [&](float (&v)[4]) {
         float t[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = sa * pn[c] + sb * pn[4 + c];
+        for (int c = 0; c < 4; ++c) t[c] = __builtin_fmaf(sx, pn[4 + c], pn[c]);
         v[0] = t[0] - t[2];
         v[1] = t[1] + t[2];
         v[2] = t[2] - t[1];
