@@ -699,24 +699,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int st = 0; st < KR; ++st) load_b(st, bw[st]);
   __syncthreads();
-  // The group loop, compiled once per wave: B^T row i combines patch rows (ra, rb) with signs (+-1), t = sa d[ra] +
-  // sb d[rb]; with the wave's row a compile-time constant that is one add or subtract per value instead of a
-  // multiply and a multiply-add (the products by +-1 are exact: the same values either way; -2..-15 % per layer).
-  // Each copy contains the band's barriers: every wave takes exactly one copy and passes the same barriers in the
-  // same order and number as the others (s_barrier counts the workgroup's waves); the probes' v(S) hashes guard
-  // the equivalence with the runtime-sign form this replaced.
-  auto groups = [&](auto wtag) __attribute__((always_inline)) {
-  constexpr int WIC = decltype(wtag)::value;
-  constexpr int ra = (WIC == 0) ? 0 : 1;
-  constexpr int rb = (WIC == 3) ? 3 : 2;
-  const int drow = (rb - ra) * ROWP;
+  // B^T row i combines two patch rows: t = d[ry] + sx d[rx] (row 0: d0 - d2, 1: d1 + d2, 2: d2 - d1, 3: d1 - d3),
+  // one fused multiply-add by +-1 per value (exact product, one rounding: the bits of the add or subtract).  This
+  // replaced per-wave compiled copies of the group loop (compile-time signs, same instruction count), whose
+  // barriers sat in wave-divergent code; now every barrier is in code all waves share.
+  const int ry = (wi == 0) ? 0 : (wi == 2) ? 2 : 1;
+  const int rx = (wi == 3) ? 3 : (wi == 2) ? 1 : 2;
+  const float sx = (wi == 1) ? 1.0f : -1.0f;
+  const int drow = (rx - ry) * ROWP;
+  {
   // The QUAD group's GEMMs (4 tiles x 64 channels per transform point, K = CI) on 4x4x1 MFMAs: lane 4 b + i
   // supplies tile i's V (the same value in all 16 blocks), lane = output channel supplies U; the wave's 4 transform
   // points are 4 accumulators.  U streams from L2 in chunks of QC channels, the next chunk in flight.
   auto quad_group = [&](int t0, fvec4 (&q)[4]) __attribute__((always_inline)) {
     const int tile = t0 + (lane & 3);
     const int tyl = tile / TXT, tx = tile % TXT;
-    const float* dpa = in_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP;
+    const float* dpa = in_s + ((2 * tyl + ry) * LC + 2 * tx) * CIP;
     const float* Uq = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + (lane & (CO - 1));
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) q[jj] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -736,8 +734,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         float t[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float da = d0[c * CIP], db = d0[drow + c * CIP];
-          t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+          t[c] = __builtin_fmaf(sx, d0[drow + c * CIP], d0[c * CIP]);
         }
         float v[4];
         v[0] = t[0] - t[2];
@@ -773,7 +770,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     } else {
     const int tile = min(16 * g + tl, ntile - 1);
     const int tyl = tile / TXT, tx = tile % TXT;
-    const float* dpa = in_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP + kq;
+    const float* dpa = in_s + ((2 * tyl + ry) * LC + 2 * tx) * CIP + kq;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
@@ -785,8 +782,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float t[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float da = d0[c * CIP], db = d0[drow + c * CIP];
-        t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+        t[c] = __builtin_fmaf(sx, d0[drow + c * CIP], d0[c * CIP]);
       }
       float v[4];
       v[0] = t[0] - t[2];
@@ -910,12 +906,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     run_group(g, IntC<0>{});
   }
   if constexpr (QUAD) run_group(NG - 1, IntC<1>{});
-  };
-  switch (wi) {  // wave-uniform
-    case 0: groups(IntC<0>{}); break;
-    case 1: groups(IntC<1>{}); break;
-    case 2: groups(IntC<2>{}); break;
-    default: groups(IntC<3>{}); break;
   }
 
 }
