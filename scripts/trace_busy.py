@@ -6,13 +6,19 @@ import sys
 
 iv = []
 per = {}
+per_grid = {}  # (kernel, grid): a kernel launched by several legs of one command (different batch shapes) apart
 with open(sys.argv[1]) as f:
-    for r in csv.DictReader(f):
+    rd = csv.DictReader(f)
+    gcols = [c for c in rd.fieldnames if c.startswith("Grid_Size")]
+    for r in rd:
         s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         iv.append((s_, e_))
         k = r["Kernel_Name"].replace("(anonymous namespace)::", "")[:60]
         n, t = per.get(k, (0, 0))
         per[k] = (n + 1, t + e_ - s_)
+        g = "x".join(r[c] for c in gcols)
+        n, t = per_grid.get((k, g), (0, 0))
+        per_grid[(k, g)] = (n + 1, t + e_ - s_)
 iv.sort()
 span = iv[-1][1] - iv[0][0]
 busy, cur_s, cur_e = 0, iv[0][0], iv[0][1]
@@ -34,3 +40,6 @@ for hi in edges:
     lo = hi
 for k, (n, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:16]:
     print(f"  {k:60s} {n:8d} {t / 1e9:8.2f} s  avg {t / n / 1e3:9.1f} us")
+print("by launch grid (kernel, grid size):")
+for (k, g), (n, t) in sorted(per_grid.items(), key=lambda kv: -kv[1][1])[:24]:
+    print(f"  {k:60s} {g:>20s} {n:8d} {t / 1e9:8.2f} s  avg {t / n / 1e3:9.1f} us")
