@@ -107,3 +107,20 @@ def test_cifar_table_puts_conv1_on_its_hbm_roof():
     assert c1["mfma_rate"]["achieved"] == pytest.approx(10000 * FLOP_PER_SAMPLE["conv1_fwd"] / 0.002 / 1e12, abs=0.01)
     assert tab["conv1_wgrad"]["bound"] == "hbm" and tab["conv4_fwd"]["bound"] == "mfma"
     assert tab["dense5_bwd"]["bound"] == "hbm"
+
+
+def test_tutorial_leg_is_the_reference_notebook_workload():
+    """bench.py's tutorial leg (vs_baseline against the reference's one published timing) runs the notebook's
+    experiment: notebooks/tutorials/Tutorial-2_Add_contributivity_measurement.ipynb prints the partner split of its
+    Scenario(3, [0.001, 0.699, 0.3], MNIST, epoch_count=10, minibatch_count=3) as 43 / 30573 / 13122 samples
+    (output lines 546-549) and its time, 1525.8 s for the 7 coalitions of exact Shapley.  The same split comes out
+    of this package's split_data on the synthetic MNIST at the full sizes."""
+    import bench
+    from mplc.dataset import Mnist
+    from mplc.scenario import Scenario
+    assert (bench.REFERENCE_TUTORIAL_S, bench.REFERENCE_TUTORIAL_COALITIONS) == (1525.8, 7)
+    sc = Scenario(3, [0.001, 0.699, 0.3], dataset=Mnist(synthetic=True, signal=0.2), epoch_count=10,
+                  minibatch_count=3).provision()
+    assert [len(p.y_train) for p in sc.partners_list] == [43, 30573, 13122]
+    # batch size = rows / (minibatch_count * gradient_updates_per_pass_count 8), at least 1
+    assert [p.batch_size for p in sc.partners_list] == [1, 1273, 546]
