@@ -535,7 +535,7 @@ def bench_train(args, rank, world):
     reserve = ((0 if args.no_shapley_agg else 10) + (25 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
                + (0 if args.no_cifar else CIFAR_SUBLEG_S / world + 15 + (15 if world == 1 else 0))
                + (0 if args.no_titanic else 15 + (12 if world == 1 and not args.no_cpu_baseline else 0))
-               + (0 if args.no_tutorial else 20))
+               + (0 if args.no_tutorial else 25))
     steps, warm, wall, c, per_step = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
@@ -951,6 +951,10 @@ def bench_titanic(args, rank, world, sub=False):
 # Tutorial-2_Add_contributivity_measurement.ipynb, exact "Shapley values" on MNIST, 3 partners [0.001, 0.699, 0.3],
 # E=10, M=3 (7 coalitions): "Computation time" 1525.8 s on a Colab GPU (model not printed), real MNIST
 REFERENCE_TUTORIAL_S, REFERENCE_TUTORIAL_COALITIONS = 1525.8, 7
+# and Tutorial-1_Run_your_first_scenario.ipynb: one FedAvg fit of the grand coalition, MNIST at 10 % (partners
+# 874 / 2186 / 1312 rows), [0.2, 0.5, 0.3], E=10, M=3: "Training and evaluation on multiple partners: done.
+# (179.283 seconds)" (per-epoch validation and the final test evaluation included)
+REFERENCE_TUTORIAL1_FIT_S = 179.283
 
 
 def bench_tutorial(args, rank, world, sub=False):
@@ -978,6 +982,26 @@ def bench_tutorial(args, rank, world, sub=False):
                                                   max_steps=3 if sub else None, warmup=1)
     value = c.first_charac_fct_calls_count * steps / wall
     ref = REFERENCE_TUTORIAL_COALITIONS / REFERENCE_TUTORIAL_S
+    # Tutorial-1's timed fit: the grand coalition's FedAvg learning with its history (per-epoch validation, final
+    # test evaluation), as Scenario.run() starts; a warm-up, then the median of three
+    sc1 = Scenario(3, [0.2, 0.5, 0.3], dataset=Mnist(synthetic=True, signal=0.2), epoch_count=10, minibatch_count=3,
+                   dataset_proportion=0.1).provision()
+    sc1.engine = CoalitionEngine.for_scenario(sc1)
+
+    def fit_once():
+        mpl = sc1.multi_partner_learning_approach(sc1, is_save_data=False, record_history=True)
+        mpl.fit()
+        torch.cuda.synchronize()
+        return mpl
+
+    fit_once()
+    fit_s = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        mpl1 = fit_once()
+        fit_s.append(time.perf_counter() - t0)
+    fit_med = sorted(fit_s)[1]
+    sc1.engine.release()
     out = {"metric": "coalition v(S) evals/sec (reference Tutorial-2: MNIST exact Shapley, 3 partners, E=10, M=3)",
            "value": round(value, 4), "unit": "coalition evals/s", "n_gpus": world, "steps": steps, "warmup": warm,
            "ms_per_step": round(wall * 1000 / steps, 1), "higher_is_better": True, "scaling": "strong",
@@ -993,7 +1017,16 @@ def bench_tutorial(args, rank, world, sub=False):
                       "per_step_ms": [round(t * 1000, 1) for t in per_step],
                       "baseline": {"value": round(ref, 5), "unit": "coalition evals/s",
                                    "source": "the tutorial notebook's printed computation time, 1525.8 s for 7 "
-                                             "coalitions on a Colab GPU (BASELINE.md section 1)"}}}
+                                             "coalitions on a Colab GPU (BASELINE.md section 1)"},
+                      "tutorial1_fit": {"seconds": round(fit_med, 4), "runs_s": [round(t, 4) for t in fit_s],
+                                        "reference_s": REFERENCE_TUTORIAL1_FIT_S,
+                                        "speedup": round(REFERENCE_TUTORIAL1_FIT_S / fit_med, 1),
+                                        "batch_size": [p.batch_size for p in sc1.partners_list],
+                                        "test_accuracy": round(float(mpl1.history.score), 4),
+                                        "workload": "Tutorial-1_Run_your_first_scenario.ipynb: one FedAvg fit of "
+                                                    "the grand coalition, MNIST-shaped at 10 % (874 / 2186 / 1312 "
+                                                    "rows), E=10, M=3, with per-epoch validation and the final test "
+                                                    "evaluation"}}}
     return out
 
 

@@ -124,3 +124,8 @@ def test_tutorial_leg_is_the_reference_notebook_workload():
     assert [len(p.y_train) for p in sc.partners_list] == [43, 30573, 13122]
     # batch size = rows / (minibatch_count * gradient_updates_per_pass_count 8), at least 1
     assert [p.batch_size for p in sc.partners_list] == [1, 1273, 546]
+    # Tutorial-1_Run_your_first_scenario.ipynb (the leg's timed grand-coalition fit, 179.283 s): its printed split
+    assert bench.REFERENCE_TUTORIAL1_FIT_S == 179.283
+    sc1 = Scenario(3, [0.2, 0.5, 0.3], dataset=Mnist(synthetic=True, signal=0.2), epoch_count=10, minibatch_count=3,
+                   dataset_proportion=0.1).provision()
+    assert [len(p.y_train) for p in sc1.partners_list] == [874, 2186, 1312]
