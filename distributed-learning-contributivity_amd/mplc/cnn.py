@@ -711,6 +711,46 @@ class CnnBatchTrainer:
             eng.stats["test_eval_s"] = eng.stats.get("test_eval_s", 0.0) + time.perf_counter() - t0
         return correct / float(eng.y_test_d.numel()), epochs_done
 
+    def run_concurrent(self, parts, epochs):
+        """Independent lockstep batches (`parts`: lists of coalitions) trained step by step interleaved, each on
+        its own HIP stream, so that their kernels overlap on the device (the CIFAR step's ~0.3 ms kernels leave
+        tails and launch gaps a second batch fills).  No early stopping, history, kept models or
+        kernel timer (CoalitionEngine.evaluate falls back to run() for those).  v(S) depends only on (S, seed):
+        every value is the one the same coalition gets in any other batch.  Returns the test accuracies per
+        part."""
+        import torch
+        eng = self.eng
+        dev = eng.device
+        main = torch.cuda.current_stream(dev)
+        streams = [torch.cuda.Stream(device=dev) for _ in parts]
+        sts = []
+        for coal, sm in zip(parts, streams):
+            sm.wait_stream(main)  # the data and anything queued before on the caller's stream
+            with torch.cuda.stream(sm):
+                sts.append(self.prepare(coal, epochs))
+        stats = eng.stats
+        for s in range(max(st.total_steps for st in sts)):
+            for st, sm in zip(sts, streams):
+                if s >= st.total_steps:
+                    continue
+                with torch.cuda.stream(sm):
+                    stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
+                    stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(
+                        np.sum(st.kind_host != REP_IDLE))
+                    st.step(s)
+                    if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                        st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
+        out = []
+        for st, sm in zip(sts, streams):
+            with torch.cuda.stream(sm):
+                glob = st.finalize()
+                c_end, _ = self._evaluate(glob, list(range(st.C)), eng.x_test_d, eng.y_test_d)  # syncs sm
+            out.append(c_end / float(eng.y_test_d.numel()))
+        for sm in streams:
+            main.wait_stream(sm)
+        self.last_es_trace = [[] for st in sts for _ in range(st.C)]
+        return out
+
     def _final_correct(self, st, cis):
         """Test hits of the final models of stopped coalitions `cis` of batch `st` (a FedAvg coalition's model
         is its coalition row, a singleton's its replica row)."""

@@ -96,6 +96,8 @@ class CoalitionEngine:
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): in-stream HIP events around the step kernels
+        # opt-in: lockstep batches split over this many HIP streams (MPLC_CONCURRENT_BATCHES, default 1 = off)
+        self.concurrent_batches = max(1, int(os.environ.get("MPLC_CONCURRENT_BATCHES", "1")))
         # FedAvg rounds leave the large dense layer out of the broadcast (the next round's first step reads it
         # from the coalition row); False broadcasts every layer (the plain copy-back, for A/B tests)
         self.bcast_skip = True
@@ -175,6 +177,28 @@ class CoalitionEngine:
         torch.cuda.empty_cache()
 
     supports_history = True
+    # Lockstep batches trained at once on separate HIP streams (CnnBatchTrainer.run_concurrent): 1 = off.  A
+    # batch of at least 2 * CONCURRENT_MIN_COALITIONS coalitions is split into that many cost-balanced parts.
+    concurrent_batches = 1
+    CONCURRENT_MIN_COALITIONS = 8
+
+    def _concurrent_ok(self, coal, E, es, history, return_models):
+        from .cnn import PATIENCE
+        return (self.concurrent_batches > 1 and len(coal) >= 2 * self.CONCURRENT_MIN_COALITIONS
+                and not (es and E > PATIENCE) and history is None and not return_models
+                and self.profiler is None and self.approach == "fedavg"
+                and hasattr(self.trainer, "run_concurrent"))
+
+    def _run_concurrent(self, coal, E):
+        from .parallel import coalition_cost, lpt_shard
+        parts = [p for p in lpt_shard([coalition_cost(c, self.partner_sizes) for c in coal], self.concurrent_batches)
+                 if p]
+        accs = self.trainer.run_concurrent([[coal[i] for i in p] for p in parts], E)
+        s = np.zeros(len(coal))
+        for p, a in zip(parts, accs):
+            s[p] = a
+        self.trainer.last_es_trace = [[] for _ in coal]
+        return s, np.full(len(coal), E, dtype=np.int64)
 
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
                  record_history=False, return_models=False):
@@ -198,7 +222,10 @@ class CoalitionEngine:
             history = {}
         for batch in self.plan_batches(coalitions):
             coal = [coalitions[i] for i in batch]
-            s, e = self.trainer.run(coal, E, es, history=history, keep_models=return_models)
+            if self._concurrent_ok(coal, E, es, history, return_models):
+                s, e = self._run_concurrent(coal, E)
+            else:
+                s, e = self.trainer.run(coal, E, es, history=history, keep_models=return_models)
             scores[batch] = s
             epochs_done[batch] = e
             for i, tr in zip(batch, getattr(self.trainer, "last_es_trace", [[]] * len(batch))):
