@@ -714,32 +714,45 @@ class CnnBatchTrainer:
     def run_concurrent(self, parts, epochs):
         """Independent lockstep batches (`parts`: lists of coalitions) trained step by step interleaved, each on
         its own HIP stream, so that their kernels overlap on the device (the CIFAR step's ~0.3 ms kernels leave
-        tails and launch gaps a second batch fills).  No early stopping, history, kept models or
-        kernel timer (CoalitionEngine.evaluate falls back to run() for those).  v(S) depends only on (S, seed):
+        tails and launch gaps a second batch fills).  No early stopping, history or kept models
+        (CoalitionEngine.evaluate falls back to run() for those); with a kernel timer on, the parts run in turn.  v(S) depends only on (S, seed):
         every value is the one the same coalition gets in any other batch.  Returns the test accuracies per
         part."""
         import torch
         eng = self.eng
         dev = eng.device
         main = torch.cuda.current_stream(dev)
-        streams = [torch.cuda.Stream(device=dev) for _ in parts]
+        # the same side streams for every batch: the caching allocator keeps its blocks per stream, so fresh streams
+        # would make every lockstep batch allocate its buffers anew
+        pool = getattr(self, "_side_streams", [])
+        while len(pool) < len(parts):
+            pool.append(torch.cuda.Stream(device=dev))
+        self._side_streams = pool
+        streams = pool[:len(parts)]
         sts = []
         for coal, sm in zip(parts, streams):
             sm.wait_stream(main)  # the data and anything queued before on the caller's stream
             with torch.cuda.stream(sm):
                 sts.append(self.prepare(coal, epochs))
         stats = eng.stats
-        for s in range(max(st.total_steps for st in sts)):
-            for st, sm in zip(sts, streams):
-                if s >= st.total_steps:
-                    continue
-                with torch.cuda.stream(sm):
-                    stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
-                    stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(
-                        np.sum(st.kind_host != REP_IDLE))
-                    st.step(s)
-                    if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
-                        st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
+        progress = getattr(eng, "progress", None)
+        if progress is not None:  # batch start, as run() reports it (the bench's in-stream timer samples batches)
+            progress(0, max(st.total_steps for st in sts), sum(st.R for st in sts))
+        # a batch the kernel timer samples runs its parts one after the other: its kernel times are not overlapped
+        groups = [[i] for i in range(len(sts))] if eng.profiler is not None else [list(range(len(sts)))]
+        for grp in groups:
+            for s in range(max(sts[i].total_steps for i in grp)):
+                for i in grp:
+                    st, sm = sts[i], streams[i]
+                    if s >= st.total_steps:
+                        continue
+                    with torch.cuda.stream(sm):
+                        stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
+                        stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(
+                            np.sum(st.kind_host != REP_IDLE))
+                        st.step(s)
+                        if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                            st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
         out = []
         for st, sm in zip(sts, streams):
             with torch.cuda.stream(sm):
