@@ -96,11 +96,10 @@ class CoalitionEngine:
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): in-stream HIP events around the step kernels
-        # lockstep batches split over this many HIP streams (MPLC_CONCURRENT_BATCHES overrides): 2 for the CIFAR10
-        # trainer, whose ~0.3 ms kernels leave room for a second batch (config #4 TMCS run +7 %), 1 (off) for MNIST
-        # (+1 % on its probe, not worth halving its 5120-replica launches)
-        self.concurrent_batches = max(1, int(os.environ.get("MPLC_CONCURRENT_BATCHES",
-                                                            "2" if model == "cifar10_cnn" else "1")))
+        # lockstep batches split over this many HIP streams (MPLC_CONCURRENT_BATCHES; default 1 = off): 2 makes the
+        # CIFAR10 config #4 TMCS run +7 %, but the bench's sampled kernel accounting of batches run
+        # in parts is not right yet, so it is opt-in
+        self.concurrent_batches = max(1, int(os.environ.get("MPLC_CONCURRENT_BATCHES", "1")))
         # FedAvg rounds leave the large dense layer out of the broadcast (the next round's first step reads it
         # from the coalition row); False broadcasts every layer (the plain copy-back, for A/B tests)
         self.bcast_skip = True

@@ -22,7 +22,7 @@ def _engine(model):
 @pytest.mark.parametrize("model", ["cifar10", "mnist"])
 def test_two_streams_bit_identical(model):
     eng = _engine(model)
-    assert eng.concurrent_batches == (2 if model == "cifar10" else 1)  # the defaults
+    assert eng.concurrent_batches == 1  # opt-in
     coals = [c for k in range(1, 7) for c in itertools.combinations(range(6), k)][:40]
     eng.concurrent_batches = 1
     one = eng.evaluate(coals)
