@@ -777,11 +777,16 @@ def bench_cifar(args, rank, world, sub=False):
     kernels = cifar_kernel_table(timer, units) if not args.no_kernel_timer else {}
     algorithmic_all = None
     if stash_all is not None and stash_all.stash:
+        from mplc.cifar import compulsory_bytes
         ua = eng.model_impl.algorithmic_units(stash_all.stash)
         n_all = len(stash_all.stash)  # one launch of every training kernel per step
         algorithmic_all = {"launches": n_all, "samples_per_launch": ua["samples"] / n_all,
-                           **{k.replace("_bytes", "_kernel"): v / n_all for k, v in ua.items() if k.endswith("_bytes")}}
-        stash_all.stash = []
+                           **{k.replace("_bytes", "_kernel"): v / n_all for k, v in ua.items() if k.endswith("_bytes")},
+                           # every kernel's compulsory bytes (mplc.cifar.compulsory_bytes), totals over the run's
+                           # training steps and evaluations, beside the counters' totals in scripts/pmc_traffic.py
+                           "compulsory": compulsory_bytes(stash_all.stash, stash_all.evals),
+                           "evaluations": len(stash_all.evals)}
+        stash_all.stash, stash_all.evals = [], []
     kern_ms = timer.total_ms(args.cifar_profile_kernel)
     launches = timer.launches(args.cifar_profile_kernel)
     samples = eng.stats["samples"] - max(0, s0[0])

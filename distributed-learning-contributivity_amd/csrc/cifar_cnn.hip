@@ -1386,8 +1386,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (j_begin >= j_end) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wi = wave;
+  const int wi = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the row's signs below live in SGPRs
   const int tl = lane & 15, kq = lane >> 4;
+  // The wave's transform row as data (round 6: one loop for all waves, every barrier in code all waves share; round 5
+  // compiled the sample loop once per wave with its barriers inside a wave-uniform switch).  V's row i of B^T d B is
+  // s_a d[ra] + s_b d[rb], written as ONE fma by +-1 (the correctly rounded value of the same two exact terms: the
+  // same bits as an add / subtract): t = fmaf(sq, d[tq], d[tp]).  D's row i of A dY (y0 | y0 + y1 | y0 - y1 | -y1)
+  // likewise as fmaf(c, y[zq], y[zp]) with c = 0 for rows 0 and 3.  Row 3 computes -V and -D instead of V and D
+  // (d3 - d1 and y1): every product V D is unchanged (a sign flip is exact on both factors), and the zero products
+  // of c = 0 never reach a result (the accumulators start at +0; adding +-0 leaves a sum unchanged), so the
+  // weight gradients are bit-identical to the per-wave copies.
+  const int tp = wi;                                                     // + row of B^T: 0 | 1 | 2 | 3
+  const int tq = (wi <= 1) ? 2 : 1;                                      // the other:    2 | 2 | 1 | 1
+  const float sq = (wi == 1) ? 1.0f : -1.0f;
+  const float cz = (wi == 1) ? 1.0f : ((wi == 2) ? -1.0f : 0.0f);       // A's row: y[zp] + cz y[zq]
+  const int zpo = (wi == 3) ? ZC * COP : 0;                              // offsets of the y rows zp / zq in z_s
+  const int zqo = (wi == 3) ? 0 : ZC * COP;
   fvec4 acc[4][NH][NCG];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj)
@@ -1396,14 +1410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fvec4 gb = fvec4{0.0f, 0.0f, 0.0f, 0.0f};  // db partial of channels 4 * (tid % (CO / 4)) .. + 3
-  // the sample loop compiled once per wave (as the group loop of wino_kernel, and with the same barrier argument):
-  // the wave's transform row fixes the signs of B^T and A, so V and D take adds / subtracts / moves instead of
-  // multiplies by 0 / +-1
-  auto samples = [&](auto wtag) __attribute__((always_inline)) {
-  constexpr int WIC = decltype(wtag)::value;
-  constexpr int ra = (WIC == 0) ? 0 : 1;
-  constexpr int rb = (WIC == 3) ? 3 : 2;
-  const int drow = (rb - ra) * XROW;
+  const int drow = (tq - tp) * XROW;
   // staging of (sample, band) in two halves: the global loads into registers, then the LDS images.  PIPE: the
   // next band's loads are issued right after this band's LDS stores, so that they land during this band's MFMAs
   // (the same values in the same places: bit-identical); otherwise loads and stores back to back.
@@ -1513,14 +1520,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int tc = ok ? tile : 0;
         const int tyl = tc / TX, tx = tc % TX;
         float va[NH][4];
-        const float* d0 = x_s + ((2 * tyl + ra) * LC + 2 * tx) * CIP + tl;
+        const float* d0 = x_s + ((2 * tyl + tp) * LC + 2 * tx) * CIP + tl;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
           float t[4];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float da = d0[c * CIP + 16 * h], db = d0[drow + c * CIP + 16 * h];
-            t[c] = (WIC == 2 ? -da : da) + (WIC == 0 || WIC == 3 ? -db : db);
+            t[c] = fmaf(sq, db, da);
           }
           va[h][0] = ok ? t[0] - t[2] : 0.0f;
           va[h][1] = ok ? t[1] + t[2] : 0.0f;
@@ -1531,22 +1538,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const float* z0 = z_s + ((2 * tyl) * ZC + 2 * tx) * COP + tl;
 #pragma unroll
         for (int cg = 0; cg < NCG; ++cg) {
-          const float y00 = z0[16 * cg], y01 = z0[COP + 16 * cg];
-          const float y10 = z0[ZC * COP + 16 * cg], y11 = z0[ZC * COP + COP + 16 * cg];
-          float r0, r1;  // row i of A dY
-          if constexpr (WIC == 0) {
-            r0 = y00;
-            r1 = y01;
-          } else if constexpr (WIC == 1) {
-            r0 = y00 + y10;
-            r1 = y01 + y11;
-          } else if constexpr (WIC == 2) {
-            r0 = y00 - y10;
-            r1 = y01 - y11;
-          } else {
-            r0 = -y10;
-            r1 = -y11;
-          }
+          const float yp0 = z0[zpo + 16 * cg], yp1 = z0[zpo + COP + 16 * cg];
+          const float yq0 = z0[zqo + 16 * cg], yq1 = z0[zqo + COP + 16 * cg];
+          const float r0 = fmaf(cz, yq0, yp0), r1 = fmaf(cz, yq1, yp1);  // row i of A dY (row 3: its negation)
           db[cg][0] = r0;
           db[cg][1] = r0 + r1;
           db[cg][2] = r0 - r1;
@@ -1560,13 +1554,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int cg = 0; cg < NCG; ++cg) acc[jj][h][cg] = mfma16(va[h][jj], db[cg][jj], acc[jj][h][cg]);
       }
     }
-  }
-  };
-  switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
-    case 0: samples(IntC<0>{}); break;
-    case 1: samples(IntC<1>{}); break;
-    case 2: samples(IntC<2>{}); break;
-    default: samples(IntC<3>{}); break;
   }
   // inverse transform dW[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]; lane holds
   // ci 16 h + 4 kq + rr (of the chunk), co 16 cg + tl

@@ -79,8 +79,19 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
     }
   };
   // GEMM roles: wave = transform row i; lane (tl = lane & 15: ci / co in a group of 16, kq = lane >> 4: tile)
-  const int wi = wave;
+  const int wi = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the row's signs below live in SGPRs
   const int tl = lane & 15, kq = lane >> 4;
+  // The wave's transform row as data (round 6: one loop for all waves, every barrier in code all waves share).
+  // Row i of B^T takes patch rows ra, rb: t = s_a d[ra] + s_b d[rb], written as ONE fma by +-1 on the row whose sign
+  // is + (tp) and the other (tq): fmaf(sq, d[tq], d[tp]) is the correctly rounded s_a d[ra] + s_b d[rb], the same bits
+  // as round 5's per-wave add / subtract.  Row i of A gives delta's row dy the factor A[i][dy] in {0, +-1}: v times
+  // that factor is v, -v or a zero, and a zero's sign never reaches a result (the MFMA accumulators start at +0 and
+  // a product of +-0 leaves a sum unchanged), so v(S) is bit-identical to the per-wave copies.
+  const int tp = (wi == 0) ? 0 : ((wi == 2) ? 2 : 1);   // the + row:  0 | 1 | 2 | 1
+  const int tq = (wi == 0) ? 2 : ((wi == 2) ? 1 : ((wi == 3) ? 3 : 2));  // the other: 2 | 2 | 1 | 3
+  const float sq = (wi == 1) ? 1.0f : -1.0f;
+  const float fa0 = (wi == 3) ? 0.0f : 1.0f;                             // A[i][0]
+  const float fa1 = (wi == 0) ? 0.0f : ((wi == 1) ? 1.0f : -1.0f);       // A[i][1]
   fvec4 acc[4][2][4];  // [j][ci half][co group]
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj)
@@ -90,17 +101,6 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   fetch(j_begin, 0);
   fetch_img(j_begin);
-  // The sample loop compiled once per wave: wave i's row of B^T (patch rows ra, rb with signs) and A's row i
-  // (delta's row dy with a factor 0 / +-1) are compile-time constants, so the signs fold into adds / subtracts
-  // (products by +-1 are exact: the same values as a runtime-sign loop, and -3 % kernel time).  Each copy contains
-  // the band loop's barriers: every wave takes exactly one copy and passes the same barriers, in the same order and
-  // number, as the others (s_barrier counts the workgroup's waves).  Specialising only the barrier-free k-step loop
-  // instead (a wave-uniform switch per band) measured +2.7 % on this kernel and a scalar (readfirstlane) dispatch
-  // spilled 146 registers, so the copies stay whole; the probe's v(S) hash guards the equivalence.
-  auto samples = [&](auto wtag) __attribute__((always_inline)) {
-  constexpr int WIC = decltype(wtag)::value;
-  constexpr int ra = (WIC == 0) ? 0 : 1;
-  constexpr int rb = (WIC == 3) ? 3 : 2;
   for (int j = j_begin; j < j_end; ++j) {
     for (int band = 0; band < 6; ++band) {
       __syncthreads();  // previous band's readers (a1_s, vq_s; and img_s by its staging) done
@@ -163,9 +163,9 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const int tb = 4 * st + kq;
         const int wr = tb / PL, wc = tb % PL;
         // V: B^T d B of the tile's 4x4 conv1 patch (rows 2*wr .., columns 2*wc ..), channels tl, 16 + tl
-        const fvec2* d0 = reinterpret_cast<const fvec2*>(a1_s + ((2 * wr + ra) * A1 + 2 * wc) * WG_CS) + tl;
-        const int drow = (rb - ra) * A1 * (WG_CS / 2);
-        fvec2 pa[4], pb[4];  // rows ra, rb of the patch, columns c: (ci tl, ci 16 + tl)
+        const fvec2* d0 = reinterpret_cast<const fvec2*>(a1_s + ((2 * wr + tp) * A1 + 2 * wc) * WG_CS) + tl;
+        const int drow = (tq - tp) * A1 * (WG_CS / 2);
+        fvec2 pa[4], pb[4];  // rows tp, tq of the patch, columns c: (ci tl, ci 16 + tl)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           pa[c] = d0[c * (WG_CS / 2)];
@@ -176,8 +176,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int ch = 0; ch < 2; ++ch) {
           float t[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            t[c] = (WIC == 2 ? -pa[c][ch] : pa[c][ch]) + (WIC == 0 || WIC == 3 ? -pb[c][ch] : pb[c][ch]);
+          for (int c = 0; c < 4; ++c) t[c] = fmaf(sq, pb[c][ch], pa[c][ch]);
           va[ch][0] = t[0] - t[2];
           va[ch][1] = t[1] + t[2];
           va[ch][2] = t[2] - t[1];
@@ -190,11 +189,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
           const int2 vs = vq_s[tb * WG_VS + 16 * cg + tl];
           const float v = __int_as_float(vs.x);
           const int sl = vs.y;
-          float vi;
-          if constexpr (WIC == 0) vi = (sl & 2) ? 0.0f : v;
-          else if constexpr (WIC == 1) vi = v;
-          else if constexpr (WIC == 2) vi = (sl & 2) ? -v : v;
-          else vi = (sl & 2) ? -v : 0.0f;
+          const float vi = v * ((sl & 2) ? fa1 : fa0);  // v * A[i][dy]: exact
           const bool dx = (sl & 1) != 0;
           db[cg][0] = dx ? 0.0f : vi;
           db[cg][1] = vi;
@@ -209,13 +204,6 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
             for (int cg = 0; cg < 4; ++cg) acc[jj][ch][cg] = mfma16(va[ch][jj], db[cg][jj], acc[jj][ch][cg]);
       }
     }
-  }
-  };
-  switch (wi) {  // wave-uniform; every copy passes the same barriers in the same order
-    case 0: samples(IntC<0>{}); break;
-    case 1: samples(IntC<1>{}); break;
-    case 2: samples(IntC<2>{}); break;
-    default: samples(IntC<3>{}); break;
   }
   // inverse transform dW2[ky][kx] = sum_i G^T[ky][i] P_i[kx], P_i[kx] = sum_j M[i][j] G[j][kx]: wave i folds
   // its row (P_i0 = M_i0 + .5 M_i1 + .5 M_i2, P_i1 = .5 M_i1 - .5 M_i2, P_i2 = .5 M_i1 + .5 M_i2 + M_i3), the

@@ -50,6 +50,76 @@ DIRECT_FLOP_PER_SAMPLE = {"conv1_fwd": 1024 * 32 * 27 * 2, "conv2_fwd": 900 * 32
 # floats per MPLC_CIFAR_WG_SAMPLES samples) are not counted.
 BYTES_PER_SAMPLE = {"conv1_fwd": 4 * (IMG_FLOATS + A1), "conv1_wgrad": 4 * (IMG_FLOATS + DZ1)}
 
+# Compulsory HBM bytes of EVERY training launch (set beside the FETCH + WRITE counters of the same
+# launches, scripts/pmc_traffic.py): each tensor a launch must read or write, once.  Per trained sample the
+# activations / gradients (fp32, the pool / dropout / ReLU codes one byte per element); per active replica-step the
+# Winograd weights the convolutions read (U, 16 x CI x CO: the data gradients' rotated form has the same size) and the
+# head's W6 / b6 RMSprop update; per weight-gradient split (WG_SAMPLES samples) the partial row it writes, and
+# rmsprop_small reads those partials and reads and writes W1..b4 and their accumulators.  dense5_fwd / dense5_bwd
+# keep their exact schedule-dependent count (algorithmic_units).  The stores of the dz / code tensors that the next
+# launch reads are counted on both sides, as they cross HBM twice.
+_F = 4
+_U2, _U3, _U4 = 16 * 32 * 32, 16 * 32 * 64, 16 * 64 * 64
+_W6 = H5 * 10 + 10
+_SMALL = 65664  # W1..b4 (the params prefix rmsprop_small updates; = WPART)
+SAMPLE_IO = {"conv1_fwd": _F * (IMG_FLOATS + A1), "conv2_fwd": _F * (A1 + D2) + D2, "conv3_fwd": _F * (D2 + A3),
+             "conv4_fwd": _F * (A3 + D4) + D4, "head": _F * 2 * H5 + H5,
+             "conv4_wgrad": _F * (A3 + DZ4) + D4, "conv4_dgrad": _F * (DZ4 + A3 + DZ3) + D4,
+             "conv3_wgrad": _F * (D2 + DZ3), "conv3_dgrad": _F * (DZ3 + DZ2) + D2,
+             "conv2_wgrad": _F * (A1 + DZ2) + D2, "conv2_dgrad": _F * (DZ2 + A1 + DZ1) + D2,
+             "conv1_wgrad": _F * (IMG_FLOATS + DZ1)}
+REPLICA_STEP_IO = {"conv2_fwd": _F * _U2, "conv3_fwd": _F * _U3, "conv4_fwd": _F * _U4, "conv4_dgrad": _F * _U4,
+                   "conv3_dgrad": _F * _U3, "conv2_dgrad": _F * _U2, "head": _F * 4 * _W6,
+                   "rmsprop_small": _F * 4 * _SMALL}
+SPLIT_IO = {"conv4_wgrad": _F * (36864 + 64), "conv3_wgrad": _F * (18432 + 64), "conv2_wgrad": _F * (9216 + 32),
+            "conv1_wgrad": _F * (864 + 32), "rmsprop_small": _F * _SMALL}
+# the evaluation's forward (mplc_cifar_evaluate: no dropout codes; weights per model and sample chunk)
+EVAL_SAMPLE_IO = {"conv1_fwd": _F * (IMG_FLOATS + A1), "conv2_fwd": _F * (A1 + D2), "conv3_fwd": _F * (D2 + A3),
+                  "conv4_fwd": _F * (A3 + D4), "dense5_fwd": _F * (D4 + H5)}
+EVAL_CHUNK_IO = {"conv2_fwd": _F * _U2, "conv3_fwd": _F * _U3, "conv4_fwd": _F * _U4, "dense5_fwd": _F * (D4 * H5 + H5)}
+# rocprofv3 kernel names (template instances, csrc/cifar_cnn.hip CONV* macros) -> the step's launch names
+KERNEL_NAME_PREFIX = (("conv_kernel<32, 32, 3, 32", "conv1_fwd"), ("wino_wl_kernel<32, 32, 32, 32", "conv2_fwd"),
+                      ("wino_kernel<15, 15, 32, 64", "conv3_fwd"), ("wino_kernel<15, 15, 64, 64", "conv4_fwd"),
+                      ("dense5_fwd16_kernel", "dense5_fwd"), ("dense5_fwd_kernel", "dense5_fwd"),
+                      ("head_kernel", "head"), ("dense5_bwd_kernel", "dense5_bwd"),
+                      ("wino_wgrad_kernel<15, 15, 64, 64", "conv4_wgrad"), ("wino_kernel<13, 13, 64, 64", "conv4_dgrad"),
+                      ("wino_wgrad_kernel<15, 15, 32, 64", "conv3_wgrad"), ("wino_kernel<15, 15, 64, 32", "conv3_dgrad"),
+                      ("wino_wgrad_kernel<32, 32, 32, 32", "conv2_wgrad"), ("wino_wl_kernel<30, 30, 32, 32", "conv2_dgrad"),
+                      ("wgrad_kernel<32, 32, 3, 32", "conv1_wgrad"), ("rmsprop_small_kernel", "rmsprop_small"),
+                      ("eval_head_kernel", "eval_head"), ("wino_u_kernel", "wino_u"), ("schedule_kernel", "schedule"))
+
+
+def launch_name(kernel):
+    """The step's launch name of a rocprofv3 kernel name (None: not a CIFAR trainer kernel)."""
+    k = kernel.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+    for prefix, name in KERNEL_NAME_PREFIX:
+        if k.startswith(prefix):
+            return name
+    return None
+
+
+def compulsory_bytes(stash, evals):
+    """Compulsory HBM bytes and launches per kernel of the stashed training steps [(cnt, opt_t, w5src)] and the
+    evaluations [(n_models, samples, chunks)] of a run (StashOnly): {name: {"bytes": total, "launches": n}}.  The
+    forward kernels' totals include the evaluation launches, which rocprofv3 reports under the same names."""
+    import torch
+    out = {k: {"bytes": 0.0, "launches": 0} for k in list(SAMPLE_IO) + ["dense5_fwd", "dense5_bwd", "rmsprop_small"]}
+    u = CifarModel.algorithmic_units(stash)
+    for cnt, _at, _src in stash:
+        c = cnt.to(torch.float64)
+        n, reps = float(c.sum()), float((c > 0).sum())
+        splits = float(torch.ceil(c / WG_SAMPLES).sum())
+        for k in out:
+            out[k]["launches"] += 1
+            out[k]["bytes"] += SAMPLE_IO.get(k, 0) * n + REPLICA_STEP_IO.get(k, 0) * reps + SPLIT_IO.get(k, 0) * splits
+    out["dense5_fwd"]["bytes"] += u.get("dense5_fwd_bytes", 0.0)
+    out["dense5_bwd"]["bytes"] += u.get("dense5_bwd_bytes", 0.0)
+    for n_models, samples, chunks in evals:
+        for k in EVAL_SAMPLE_IO:
+            out[k]["launches"] += chunks
+            out[k]["bytes"] += EVAL_SAMPLE_IO[k] * n_models * samples + EVAL_CHUNK_IO.get(k, 0) * n_models * chunks
+    return out
+
 
 class CifarTrainT(ctypes.Structure):
     _fields_ = ([("n_rep", ctypes.c_int32), ("bmax", ctypes.c_int32), ("wg_splits", ctypes.c_int32),
@@ -211,8 +281,11 @@ class CifarModel:
         ws = torch.empty(int(self.lib.mplc_cifar_eval_workspace_floats(group, chunk)), dtype=torch.float32, device=dev)
         correct = torch.zeros(C, dtype=torch.int32, device=dev)
         loss = torch.zeros(C, dtype=torch.float64, device=dev)
+        prof = eng.profiler
         for g0 in range(0, C, group):
             g = min(group, C - g0)
+            if prof is not None and hasattr(prof, "stash_eval"):  # (models, samples, chunks) of this launch group
+                prof.stash_eval(g, n, -(-n // chunk))
             _native.check(self.lib.mplc_cifar_evaluate(_native.ptr(sel[g0:g0 + g]), STRIDE, g, _native.ptr(x),
                                                        _native.ptr(y), n, chunk, _native.ptr(ws),
                                                        _native.ptr(correct[g0:g0 + g]), _native.ptr(loss[g0:g0 + g]),

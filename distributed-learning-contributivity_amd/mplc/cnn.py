@@ -336,6 +336,28 @@ class MnistModel:
         return correct.cpu().numpy().astype(np.float64), loss.cpu().numpy() / n
 
 
+def schedule_geometry(eng, coalitions, epochs, seq_mode=False):
+    """(round_len, fed_steps, total_steps) of a lockstep batch: the longest partner fit of any round (FedAvg; the
+    members' fits back to back for the sequential approaches), the FedAvg steps and the steps the batch runs."""
+    sizes, M = eng.partner_sizes, eng.minibatch_count
+    round_len, single_steps = 1, 0
+    for coal in coalitions:
+        if len(coal) == 1:
+            p = coal[0]
+            single_steps = max(single_steps, epochs * -(-sizes[p] // eng.batch_sizes[p]))
+        elif seq_mode:  # the members' fits run back to back inside a round
+            for m in range(M):
+                round_len = max(round_len, sum(-(-(eng.bounds[p][m + 1] - eng.bounds[p][m]) // eng.batch_sizes[p])
+                                               for p in coal))
+        else:
+            for p in coal:
+                b = eng.bounds[p]
+                for m in range(M):
+                    round_len = max(round_len, -(-(b[m + 1] - b[m]) // eng.batch_sizes[p]))
+    fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
+    return round_len, fed_steps, max(fed_steps, single_steps)
+
+
 class TrainBatch:
     """Device state of one lockstep batch: coalition global rows, replica rows, optimizer state, workspaces
     (model-specific parts through eng.model_impl)."""
@@ -389,24 +411,7 @@ class TrainBatch:
         for i, rp in enumerate(reps):
             self.rep_arr[i] = rp
         self.bmax = int(max(eng.batch_sizes[p] for coal in coalitions for p in coal))
-        M = eng.minibatch_count
-        round_len, single_steps = 1, 0
-        for coal in coalitions:
-            if len(coal) == 1:
-                p = coal[0]
-                single_steps = max(single_steps, epochs * -(-sizes[p] // eng.batch_sizes[p]))
-            elif seq_mode:  # the members' fits run back to back inside a round
-                for m in range(M):
-                    round_len = max(round_len, sum(-(-(eng.bounds[p][m + 1] - eng.bounds[p][m]) // eng.batch_sizes[p])
-                                                   for p in coal))
-            else:
-                for p in coal:
-                    b = eng.bounds[p]
-                    for m in range(M):
-                        round_len = max(round_len, -(-(b[m + 1] - b[m]) // eng.batch_sizes[p]))
-        self.round_len = round_len
-        self.fed_steps = epochs * M * round_len if any(len(c) > 1 for c in coalitions) else 0
-        self.total_steps = max(self.fed_steps, single_steps)
+        self.round_len, self.fed_steps, self.total_steps = schedule_geometry(eng, coalitions, epochs, seq_mode)
         if resume is not None:
             self.round_len, self.fed_steps, self.total_steps = (resume["round_len"], resume["fed_steps"],
                                                                 resume["total_steps"])
@@ -594,9 +599,10 @@ class CnnBatchTrainer:
     # compacted (CnnBatchTrainer._compact); 0 keeps every batch whole
     COMPACT_LIVE_SHARE = 0.75
 
-    def run(self, coalitions, epochs, early_stopping, history=None, keep_models=False):
+    def run(self, coalitions, epochs, early_stopping, history=None, keep_models=False, started=False):
         """Train the coalitions in lockstep; returns (test accuracies, epochs done).  With `history` (a
-        dict, one coalition only) the learning history is recorded into it (HistoryRecorder).
+        dict, one coalition only) the learning history is recorded into it (HistoryRecorder).  started: the
+        batch's start was already reported to eng.progress (run_concurrent falling back to one stream).
 
         Early stopping leaves stopped coalitions' replicas idle in the lockstep batch; when the live replicas
         drop to COMPACT_LIVE_SHARE of the batch (FedAvg, several coalitions) the stopped coalitions' final models
@@ -646,7 +652,7 @@ class CnnBatchTrainer:
                 stats["compactions"] = stats.get("compactions", 0) + 1
             stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
             stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + live_reps
-            if progress is not None and s % 30 == 0:
+            if progress is not None and s % 30 == 0 and not (started and s == 0):
                 progress(s, st.total_steps, st.R)
             if rec is not None and st.fed_steps and s % st.round_len == 0 and s < st.fed_steps:
                 vl = rec.round_start(s)  # val of the round's start model (also the ES value at minibatch 0)
@@ -715,12 +721,29 @@ class CnnBatchTrainer:
         """Independent lockstep batches (`parts`: lists of coalitions) trained step by step interleaved, each on
         its own HIP stream, so that their kernels overlap on the device (the CIFAR step's ~0.3 ms kernels leave
         tails and launch gaps a second batch fills).  No early stopping, history or kept models
-        (CoalitionEngine.evaluate falls back to run() for those); with a kernel timer on, the parts run in turn.  v(S) depends only on (S, seed):
-        every value is the one the same coalition gets in any other batch.  Returns the test accuracies per
-        part."""
+        (CoalitionEngine.evaluate falls back to run() for those).  A batch the bench's kernel timer samples (the
+        profiler set by eng.progress at the batch's start) runs as ONE lockstep batch on the caller's stream: its
+        launches are then timed without another stream's kernels overlapping them, and each launch covers the
+        whole batch, as in a single-stream run (round 5's parts run "in turn" were still concurrent on the device:
+        only their enqueueing was sequential, so every timed launch shared the GPU with the other part's).
+        v(S) depends only on (S, seed): every value is the one the same coalition gets in any other batch.
+        Returns the test accuracies per part."""
         import torch
         eng = self.eng
         dev = eng.device
+        stats = eng.stats
+        progress = getattr(eng, "progress", None)
+        if progress is not None:  # batch start, as run() reports it (the bench's in-stream timer samples batches)
+            geo = [schedule_geometry(eng, coal, epochs)[2] for coal in parts]
+            progress(0, max(geo), sum(len(c) for coal in parts for c in coal))
+        if eng.profiler is not None:
+            flat = [c for coal in parts for c in coal]
+            acc, _ = self.run(flat, epochs, False, started=True)
+            out, i = [], 0
+            for coal in parts:
+                out.append(acc[i:i + len(coal)])
+                i += len(coal)
+            return out
         main = torch.cuda.current_stream(dev)
         # the same side streams for every batch: the caching allocator keeps its blocks per stream, so fresh streams
         # would make every lockstep batch allocate its buffers anew
@@ -734,25 +757,17 @@ class CnnBatchTrainer:
             sm.wait_stream(main)  # the data and anything queued before on the caller's stream
             with torch.cuda.stream(sm):
                 sts.append(self.prepare(coal, epochs))
-        stats = eng.stats
-        progress = getattr(eng, "progress", None)
-        if progress is not None:  # batch start, as run() reports it (the bench's in-stream timer samples batches)
-            progress(0, max(st.total_steps for st in sts), sum(st.R for st in sts))
-        # a batch the kernel timer samples runs its parts one after the other: its kernel times are not overlapped
-        groups = [[i] for i in range(len(sts))] if eng.profiler is not None else [list(range(len(sts)))]
-        for grp in groups:
-            for s in range(max(sts[i].total_steps for i in grp)):
-                for i in grp:
-                    st, sm = sts[i], streams[i]
-                    if s >= st.total_steps:
-                        continue
-                    with torch.cuda.stream(sm):
-                        stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
-                        stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(
-                            np.sum(st.kind_host != REP_IDLE))
-                        st.step(s)
-                        if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
-                            st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
+        for s in range(max(st.total_steps for st in sts)):
+            for st, sm in zip(sts, streams):
+                if s >= st.total_steps:
+                    continue
+                with torch.cuda.stream(sm):
+                    stats["replica_steps"] = stats.get("replica_steps", 0) + st.R
+                    stats["replica_steps_live"] = stats.get("replica_steps_live", 0) + int(
+                        np.sum(st.kind_host != REP_IDLE))
+                    st.step(s)
+                    if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                        st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
         out = []
         for st, sm in zip(sts, streams):
             with torch.cuda.stream(sm):

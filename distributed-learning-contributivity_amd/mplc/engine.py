@@ -96,10 +96,11 @@ class CoalitionEngine:
         self.memory_budget_bytes = int(memory_budget_bytes)
         self.trainer = CnnBatchTrainer(self)
         self.profiler = None  # optional KernelTimer (bench.py): in-stream HIP events around the step kernels
-        # lockstep batches split over this many HIP streams (MPLC_CONCURRENT_BATCHES; default 1 = off): 2 makes the
-        # CIFAR10 config #4 TMCS run +7 %, but the bench's sampled kernel accounting of batches run
-        # in parts is not right yet, so it is opt-in
-        self.concurrent_batches = max(1, int(os.environ.get("MPLC_CONCURRENT_BATCHES", "1")))
+        # lockstep batches split over this many HIP streams (MPLC_CONCURRENT_BATCHES overrides): 2 for the CIFAR10
+        # model, whose ~0.3 ms step kernels leave tails and launch gaps a second batch fills (config #4 TMCS +7 %,
+        # DESIGN.md 8); 1 for MNIST (+1 % there: its 5120-replica launches already fill the chip)
+        default_streams = "2" if model == "cifar10_cnn" else "1"
+        self.concurrent_batches = max(1, int(os.environ.get("MPLC_CONCURRENT_BATCHES", default_streams)))
         # FedAvg rounds leave the large dense layer out of the broadcast (the next round's first step reads it
         # from the coalition row); False broadcasts every layer (the plain copy-back, for A/B tests)
         self.bcast_skip = True
@@ -191,6 +192,22 @@ class CoalitionEngine:
                 and self.approach == "fedavg"
                 and hasattr(self.trainer, "run_concurrent"))
 
+    def _within_budget(self, coal):
+        """Keep the device memory of a lockstep batch within the engine's budget across HIP streams.
+        The caching allocator keeps freed blocks per stream, so the blocks a two-stream batch left on the side
+        streams cannot serve a batch on the caller's stream (the bench's timed batches) and vice versa: when the
+        cached-but-unused memory plus this batch's need would pass memory_budget_bytes (what the batches may
+        use beside the resident data), the cache is returned to the driver first.  TMCS-sized batches (a few GB)
+        never trigger it."""
+        import torch
+        if self.concurrent_batches <= 1:
+            return
+        need = sum(len(c) * self.replica_bytes(max(self.batch_sizes[p] for p in c)) for c in coal)
+        idle = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        if idle > 0 and idle + need > self.memory_budget_bytes:
+            self.release()
+            self.stats["cache_releases"] = self.stats.get("cache_releases", 0) + 1
+
     def _run_concurrent(self, coal, E):
         from .parallel import coalition_cost, lpt_shard
         parts = [p for p in lpt_shard([coalition_cost(c, self.partner_sizes) for c in coal], self.concurrent_batches)
@@ -224,6 +241,7 @@ class CoalitionEngine:
             history = {}
         for batch in self.plan_batches(coalitions):
             coal = [coalitions[i] for i in batch]
+            self._within_budget(coal)
             if self._concurrent_ok(coal, E, es, history, return_models):
                 s, e = self._run_concurrent(coal, E)
             else:

@@ -109,13 +109,39 @@ class LogRegEngine:
 
     supports_history = True
     HIST_BLOCK = 2 + 4 * MAXP
+    # coalitions per mplc_lr_fedavg call: its stream-ordered workspace holds every coalition's partner fits (C x 64 x
+    # 32 doubles, 16 KB per coalition), so an exact sweep over 2^20 coalitions would ask for ~17 GB at once (ADVICE
+    # r5); each coalition's fits are independent of the others in the call, so chunks give the same values
+    CALL_COALITIONS = 32768
 
     def evaluate(self, coalitions, epoch_count=None, is_early_stopping=None, return_details=False,
                  record_history=False, return_models=False):
         """v(S) for each coalition; with record_history (one coalition) the details also hold its learning
         history (mplc/mpl_utils.py:11-27) in the layout of multi_partner_learning.History."""
-        import torch
         coalitions = [tuple(sorted(int(i) for i in c)) for c in coalitions]
+        if len(coalitions) > self.CALL_COALITIONS:
+            if record_history:
+                raise ValueError("record_history takes exactly one coalition")
+            scores, epochs, thetas = [], [], []
+            for i in range(0, len(coalitions), self.CALL_COALITIONS):
+                scores.append(self._evaluate_call(coalitions[i:i + self.CALL_COALITIONS], epoch_count,
+                                                  is_early_stopping, False, False, False))
+                epochs.append(self.last_epochs_done)
+                thetas.append(self.last_theta)
+            scores = np.concatenate(scores)
+            self.last_epochs_done, self.last_theta = np.concatenate(epochs), np.concatenate(thetas)
+            if not return_details:
+                return scores
+            out = {"scores": scores, "epochs_done": self.last_epochs_done}
+            if return_models:
+                out["models"] = [self.last_theta[ci].reshape(1, -1).copy() for ci in range(len(coalitions))]
+            return out
+        return self._evaluate_call(coalitions, epoch_count, is_early_stopping, return_details, record_history,
+                                   return_models)
+
+    def _evaluate_call(self, coalitions, epoch_count, is_early_stopping, return_details, record_history,
+                       return_models):
+        import torch
         C = len(coalitions)
         if record_history and C != 1:
             raise ValueError("record_history takes exactly one coalition")

@@ -153,10 +153,15 @@ class MultiPartnerLearning:
         from .parallel import EpochModel, sharded_evaluate
         eng = _engine(scenario)
 
-        def local(cs):  # Contributivity always builds its learners with is_early_stopping=True
-            return eng.evaluate(cs, is_early_stopping=True)
+        # Contributivity always builds its learners with is_early_stopping=True (mplc/contributivity.py:101-112),
+        # whatever the scenario's own flag: that is the flag the training below uses
+        es_flag = True
+
+        def local(cs):
+            return eng.evaluate(cs, is_early_stopping=es_flag)
         # with early stopping a coalition's cost follows its realised epochs: the LPT plan learns them per size
-        es = bool(getattr(eng, "is_early_stopping", False)) and int(getattr(eng, "epoch_count", 0)) > constants.PATIENCE
+        # (from the flag the evaluation is actually given, not the scenario's)
+        es = es_flag and int(getattr(eng, "epoch_count", 0)) > constants.PATIENCE
         model = None
         if es:
             model = getattr(eng, "epoch_model", None)

@@ -108,9 +108,13 @@ class StashOnly:
     def __init__(self, kernel):
         self.kernel = kernel  # any kernel of the model: the library records nothing (NULL events)
         self.stash = []
+        self.evals = []  # (models, samples, sample chunks) of every evaluation launch group (CifarModel.evaluate)
 
     def pair(self):
         return None, None
 
     def stash_step(self, *tensors):
         self.stash.append(tuple(t.clone() for t in tensors))
+
+    def stash_eval(self, n_models, n_samples, chunks):
+        self.evals.append((int(n_models), int(n_samples), int(chunks)))

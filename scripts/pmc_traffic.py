@@ -9,8 +9,12 @@ algorithmic bytes of the same launches when the profiled bench line carries them
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "distributed-learning-contributivity_amd"))
 
 
 def load(d, counter):
@@ -46,6 +50,28 @@ def main(fetch_dir, write_dir, bench_json, out):
             e["traffic_over_algorithmic"] = e["traffic_bytes_per_launch"] / alg[k]
             e["launches_stashed"] = alg["launches"]
     doc = {"workload": line["config"]["workload"], "source": f"{fetch_dir} + {write_dir}", "kernels": res}
+    comp = alg.get("compulsory") or {}
+    if comp:  # config #4: every launch name's counter bytes beside its compulsory bytes (mplc.cifar.compulsory_bytes)
+        from mplc.cifar import launch_name
+        by = defaultdict(lambda: [0.0, 0.0, 0, 0])
+        for k, v in f.items():
+            e = by[launch_name(k) or k]
+            e[0] += 2.0 * v
+            e[2] += nf[k]
+        for k, v in w.items():
+            e = by[launch_name(k) or k]
+            e[1] += v
+            e[3] += nw[k]
+        summ = {}
+        for name, (rd, wr, lf, lw) in sorted(by.items()):
+            rec = {"pmc_read_bytes": rd, "pmc_write_bytes": wr, "pmc_launches": max(lf, lw)}
+            c = comp.get(name)
+            if c and c["bytes"] > 0:
+                rec.update({"compulsory_bytes": c["bytes"], "compulsory_launches": c["launches"],
+                            "traffic_over_compulsory": (rd + wr) / c["bytes"]})
+            summ[name] = rec
+        doc["by_launch"] = summ
+        doc["over_1_1"] = sorted(k for k, r in summ.items() if r.get("traffic_over_compulsory", 0) > 1.1)
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -38,11 +38,25 @@ def config1_scenario(amounts, signal=0.3):
     return sc
 
 
-def config3_scenario():
+def config3_scenario(epochs=1):
     from mplc.dataset import Mnist
     from mplc.scenario import Scenario
     return Scenario(10, [0.1] * 10, dataset=Mnist(synthetic=True, signal=0.2), minibatch_count=20,
-                    gradient_updates_per_pass_count=8, epoch_count=1, is_early_stopping=False).provision()
+                    gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False).provision()
+
+
+# config #4's 20-partner CIFAR10 partition ([0.05] * 19 + [1 - 0.95]: the reference's sum check), signal 0.4, and the
+# eight coalitions of tests/test_workload_gpu.py::test_config4_learned_accuracies_vs_oracle (fixed before any run)
+CONFIG4_E2_COALS = [(2, 9, 14), (0, 7, 11, 16), (1, 4, 6, 11, 15, 19), (3, 5, 8, 10, 12), (2, 9, 14, 17),
+                    (0, 3, 5, 8, 10, 12, 13, 18), (6, 13, 17), (1, 7, 15, 18)]
+
+
+def config4_scenario(epochs=1):
+    from mplc.dataset import Cifar10
+    from mplc.scenario import Scenario
+    amounts = [0.05] * 19 + [float(1 - np.sum([0.05] * 19))]
+    return Scenario(20, amounts, dataset=Cifar10(synthetic=True, signal=0.4), minibatch_count=20,
+                    gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False).provision()
 
 
 def scenario(name):
@@ -53,6 +67,10 @@ def scenario(name):
         return config1_scenario([0.1, 0.9]), [(0,), (1,), (0, 1)]
     if name == "config3":
         return config3_scenario(), CONFIG3_COALS
+    if name == "config3_e2":  # the same partition and coalitions at E=2 (where the models have left the steep part)
+        return config3_scenario(epochs=2), CONFIG3_COALS
+    if name == "config4_e2":
+        return config4_scenario(epochs=2), CONFIG4_E2_COALS
     raise ValueError(name)
 
 
@@ -67,15 +85,27 @@ def data_crc(sc):
 
 
 def oracle_values(sc, coals, threads, precise=False, seed=0):
+    """v(S) of `coals` from the scenario's model oracle (oracle/cnn.py for MNIST, oracle/cifar_cnn.py for CIFAR10,
+    sequential like the reference) at `threads` CPU threads; precise=True: every tensor operation in fp64."""
     import torch
     from oracle import cnn as ocnn
     ds = sc.dataset
-    data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    cifar = getattr(ds, "name", "mnist") == "cifar10"
+    if cifar:
+        from oracle import cifar_cnn as occ
+        data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
+    else:
+        data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow = [p.train_idx for p in sc.partners_list]
     bs = [p.batch_size for p in sc.partners_list]
     t0 = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
+        if cifar:
+            if precise:
+                raise NotImplementedError("oracle/cifar_cnn.py coalition_value has no fp64 mode")
+            return [float(occ.coalition_value(data, prow, bs, k, seed=seed, epochs=sc.epoch_count,
+                                              M=sc.minibatch_count)[0]) for k in coals]
         return [float(ocnn.coalition_value(data, prow, bs, k, seed=seed, epochs=sc.epoch_count, M=sc.minibatch_count,
                                            precise=precise)[0]) for k in coals]
     finally:

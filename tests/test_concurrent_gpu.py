@@ -1,6 +1,7 @@
 """GPU: lockstep batches split over two HIP streams (CoalitionEngine.concurrent_batches, CnnBatchTrainer.
 run_concurrent) give every coalition the value it gets in one batch, bit for bit (v(S) depends only on (S, seed)),
-for the CIFAR10 and MNIST trainers."""
+for the CIFAR10 and MNIST trainers.  Two streams are the CIFAR10 default; a batch the bench's kernel timer samples
+runs as one lockstep batch on one stream, so its launches are timed without overlap."""
 import itertools
 
 import numpy as np
@@ -22,7 +23,7 @@ def _engine(model):
 @pytest.mark.parametrize("model", ["cifar10", "mnist"])
 def test_two_streams_bit_identical(model):
     eng = _engine(model)
-    assert eng.concurrent_batches == 1  # opt-in
+    assert eng.concurrent_batches == (2 if model == "cifar10" else 1)  # the default
     coals = [c for k in range(1, 7) for c in itertools.combinations(range(6), k)][:40]
     eng.concurrent_batches = 1
     one = eng.evaluate(coals)
@@ -31,3 +32,33 @@ def test_two_streams_bit_identical(model):
     two = eng.evaluate(coals)
     assert np.array_equal(one, two), np.nonzero(one != two)
     assert len(np.unique(one)) > 5  # trained models, not a constant (small CIFAR runs stay near chance at E=1)
+
+
+def test_timed_batch_runs_as_one_lockstep_batch():
+    """With the kernel timer switched on at the batch's start (bench.py's progress hook), a two-stream batch trains
+    as one batch: one launch of every kernel per step, each covering all the batch's replicas, the values
+    unchanged; the start is reported once."""
+    from mplc.profiling import KernelTimer
+    from mplc.cifar import KERNEL_IDS
+    from mplc.cnn import schedule_geometry
+    eng = _engine("cifar10")
+    coals = [c for k in range(1, 7) for c in itertools.combinations(range(6), k)][:40]
+    eng.concurrent_batches = 1
+    one = eng.evaluate(coals)
+    eng.concurrent_batches = 2
+    timer = KernelTimer("all", list(KERNEL_IDS), stash=True)
+    starts = []
+
+    def progress(s, total, R):
+        if s == 0:
+            starts.append((total, R))
+            eng.profiler = timer
+    eng.progress = progress
+    two = eng.evaluate(coals)
+    eng.progress, eng.profiler = None, None
+    assert np.array_equal(one, two)
+    steps = schedule_geometry(eng, [tuple(c) for c in coals], eng.epoch_count)[2]
+    assert starts == [(steps, sum(len(c) for c in coals))]
+    assert timer.launches("dense5_bwd") == steps  # one launch per step: not one per part
+    units = eng.model_impl.algorithmic_units(timer.stash)
+    assert units["samples"] == sum(eng.partner_sizes[p] for c in coals for p in c) * eng.epoch_count

@@ -112,6 +112,25 @@ def test_titanic_exact_shapley_all_1023_coalitions():
 
 
 @pytest.mark.gpu
+def test_lr_evaluate_in_chunks_equals_one_call():
+    """LogRegEngine.evaluate splits long coalition lists into calls of CALL_COALITIONS (the workspace holds every
+    coalition's partner fits: ADVICE r5); every value, epoch count and model equals the one-call result."""
+    from itertools import combinations
+    from mplc.dataset import Titanic
+    from mplc.engine import CoalitionEngine
+    from mplc.scenario import Scenario
+    sc = Scenario(10, [0.1] * 10, dataset=Titanic(synthetic=True), epoch_count=3, minibatch_count=1,
+                  is_early_stopping=False).provision()
+    eng = CoalitionEngine.for_scenario(sc)
+    coals = [c for k in range(1, 11) for c in combinations(range(10), k)]
+    one = eng.evaluate(coals, return_details=True, return_models=True)
+    eng.CALL_COALITIONS = 100
+    parts = eng.evaluate(coals, return_details=True, return_models=True)
+    assert np.array_equal(one["scores"], parts["scores"]) and np.array_equal(one["epochs_done"], parts["epochs_done"])
+    assert all(np.array_equal(a, b) for a, b in zip(one["models"], parts["models"]))
+
+
+@pytest.mark.gpu
 def test_fedavg_round_is_np_average_of_the_partner_fits():
     """E = 1, M = 1: a coalition's round-0 fits are its partners' singleton fits (same rows, same zero start, same
     code), so its model must be np.average of the singletons' models with the reference's weights, bit for bit

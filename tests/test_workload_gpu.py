@@ -5,17 +5,15 @@ M=20, G=8 (E=1 here to keep the test near 20 s; the bench runs E=2).  All 1023 c
 train as ONE lockstep batch.  Checks:
   - efficiency: sum of the Shapley values = v(N) (to 1e-12; v(empty) = 0, mplc/contributivity.py:1210-1253);
   - batch invariance: coalitions re-evaluated alone give bit-identical values to the 5120-replica batch;
-  - |S| in {1, 2} coalitions against the oracle (oracle/cnn.py, sequential like the reference): no bias
+  - |S| in {1, 2} coalitions against the oracle (oracle/cnn.py, sequential like the reference): at E=1 no bias
     (the mean SIGNED difference over eighteen coalitions - all ten singletons, eight pairs - within 1 pt of the
-    oracle's median), each within the oracle's own spread over eight CPU thread counts widened by 1 pt (10000 test
-    samples: 1 pt = 100 samples).  One epoch leaves the models in the steep part of
-    learning, where fp32 summation order alone moves a single coalition's accuracy by points: the oracle
-    against ITSELF, run with 8 vs 3 CPU threads, gives 0.9675 vs 0.9793 for (0, 9), and 0.8766 (8 threads
-    here) vs 0.8632 (16 threads on the GPU box) for (2, 7) at signal 0.2 (0.2-0.8 pt apart even at E=2),
-    and the engine's convolutions are Winograd transforms whose fp32 rounding differs from the oracle's
-    direct ones.  What IS exact is held exactly elsewhere: initial weights and sample schedule bit for bit,
-    one step's gradients and activations to 1e-4 against fp64, the Adam step, the FedAvg average, and the
-    evaluation path (tests/test_cnn_gpu.py);
+    oracle's median over eight CPU thread counts); at E=2 each of the eighteen within the oracle's range over those
+    thread counts and fp64 + 1 pt, fixed (10000 test samples: 1 pt = 100 samples).  One epoch leaves the models in
+    the steep part of learning, where every fp32 trajectory - device and oracle - forks from fp64 within two
+    rounds (profiles/r06_diag_config3.log; coalition (2, 9)'s 20 rounds are gated one by one against fp64 in
+    test_config3_coalition_2_9_round_trajectories_vs_fp64).  What IS exact is held exactly elsewhere: initial
+    weights and sample schedule bit for bit, one step's gradients and activations to 1e-4 against fp64, the Adam
+    step, the FedAvg average, and the evaluation path (tests/test_cnn_gpu.py);
   - the memo holds every coalition once (first_charac_fct_calls_count = 1023).
 Config #4 - CIFAR10 CNN, 20 partners ([0.05]*19 + [1 - 0.95], the reference's sum check), FedAvg, TMCS with
 the reference's defaults (sv_accuracy .01, alpha .95, truncation .05, numpy seed 0), E=1, M=20, G=8.  The
@@ -71,16 +69,22 @@ def test_config3_batch_invariance(mnist10, config3_sweep):
 
 
 def test_config3_small_coalitions_vs_oracle(mnist10, config3_sweep):
-    """All ten singletons and eight pairs against the oracle's own spread over summation orders: the oracle at 1, 2,
-    3, 4, 6, 8, 12 and 16 CPU threads and in fp64 (tests/golden/oracle_spread_config3.json, scripts/oracle_spread.py)
-    plus one live run at the box's thread count.  After one epoch these models sit in the steep part of learning, where
-    the summation order alone moves a coalition by up to 4 pt in the oracle itself (e.g. (0, 9): 0.858 .. 0.900 over
-    the thread counts), so a bound against ONE oracle run had to be 2 pt mean |diff| / 4 pt max (rounds 2-4).  The
-    gate now: each coalition within the references' range widened on both sides by that range
-    itself (at least 1 pt), and the mean signed difference to the oracle's median within 1 pt.  The range includes
-    fp64: partner 9's coalitions fork between precisions ((9,): 0.636 in fp64 against 0.724 .. 0.751 in fp32; (2, 9):
-    0.904 against 0.877 .. 0.887), which eight fp32 thread counts alone under-sample - the first GPU run of the
-    fp32-only gate put (2, 9) at 0.915, 1.2 pt above fp64 (profiles/r05_gpu_suite_gate_miss.log)."""
+    """E=1: no systematic bias.  All ten singletons and eight pairs of the 1023-coalition sweep: the mean signed
+    difference to the oracle's median over summation orders (the oracle at 1, 2, 3, 4, 6, 8, 12 and 16 CPU threads,
+    tests/golden/oracle_spread_config3.json, plus one live run at the box's thread count) within 1 pt.
+
+    The PER-COALITION gate lives at E=2 (test_config3_e2_accuracies_vs_oracle): after one epoch
+    every fp32 trajectory of these models - the device's and the oracle's at any thread count - leaves the fp64
+    trajectory of the same algorithm within two FedAvg rounds and ends 0.6 of the update's norm away from it
+    (scripts/diag_config3.py, profiles/r06_diag_config3.log).  Coalition (2, 9), whose device value 0.9151 sat
+    1.2 pt above every reference in round 5: per round, restarted from the device's own model, the device's error
+    against fp64 is the fp32 oracle's (ratio ~1) except in the rounds where one side meets a max-pool / ReLU near-tie
+    the other does not (rounds 7 and 11 on the device, 1, 6, 13 and 15 in the oracle: errors 1e-4 .. 5e-3 against
+    ~2e-6); the oracle's own free trajectories end at 0.876 .. 0.899 across thread counts and CPUs (the box's CPU at
+    one thread gives 0.899, the build container's 0.881), fp64 at 0.9035.  Partner 9's singleton: every fp32
+    trajectory ends at 0.742 .. 0.754 (device 0.742), fp64 at 0.636 - one basin for fp32, another for fp64, which is
+    why round 5's band, widened by the fp32 / fp64 range, spanned 35 pt and could not fail.  Summation-order forks,
+    not a kernel defect: no bound of +-1 pt per coalition holds for the oracle against itself in this regime."""
     import torch
     from spread_fixtures import load_spread, oracle_values
     c, eng = config3_sweep
@@ -89,14 +93,9 @@ def test_config3_small_coalitions_vs_oracle(mnist10, config3_sweep):
     refs = [rec["fp32"][str(t)] for t in rec["threads"]]
     refs.append(oracle_values(mnist10, coals, torch.get_num_threads()))  # the box's own summation order
     med = np.median(np.array(refs), axis=0)
-    refs.append(rec["fp64"])
-    refs = np.array(refs)
     dev = np.array([c.charac_fct_values[k] for k in coals])
-    width = np.maximum(0.01, refs.max(axis=0) - refs.min(axis=0))
-    lo, hi = refs.min(axis=0) - width, refs.max(axis=0) + width
-    print(list(zip(coals, dev.tolist(), refs.min(axis=0).tolist(), refs.max(axis=0).tolist(), rec["fp64"])))
+    print(list(zip(coals, dev.tolist(), np.min(refs, axis=0).tolist(), np.max(refs, axis=0).tolist(), rec["fp64"])))
     assert abs(np.mean(dev - med)) <= 0.01, (dev, med)  # no systematic bias
-    assert np.all((lo <= dev) & (dev <= hi)), (coals, dev, refs)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -326,23 +325,104 @@ def test_config3_round_trajectory_vs_fp64(mnist10):
     assert not bad, (bad, report)
 
 
-def test_config3_e2_accuracies_vs_oracle(mnist10):
-    """v(S) at E=2 (the bench's config #3 setting; the oracle's own run-to-run spread is 0.2-0.8 pt there) on
-    eight coalitions fixed before looking at results: mean signed difference <= 1 pt, each <= 2 pt."""
+def test_config3_coalition_2_9_round_trajectories_vs_fp64(mnist10):
+    """Coalition (2, 9), the E=1 value that sat 1.2 pt above every reference in round 5: each of
+    its 20 FedAvg rounds of epoch 0, started from the device's global model at the round's start, against
+    oracle/cnn.py fedavg_round(precise=True) - the same round (keys, batches, fresh Keras Adam per partner,
+    data-volume average) with every tensor operation in fp64.  Per round and tensor the error on the round's update,
+    ||dev - ref64|| / ||ref64 - start||, beside the fp32 oracle's (the largest over 1, 2, 3, 8 and the box's CPU
+    threads).  As for config #1's (0, 1) (tests/test_config1_gpu.py) the errors are bimodal: ~1e-6 .. 1e-4 where
+    neither side meets a near-tie, 1e-4 .. 5e-3 in the rounds where a max-pool window or a ReLU input near 0 breaks
+    the other way on one side only (profiles/r06_diag_config3.log: rounds 7 and 11 on the device, 1, 6, 13 and 15 in
+    the oracle).  Gate, per tensor on the MEDIAN round: device error <= 4x the fp32 oracle's; at most 8 of the 20
+    rounds with any tensor outside 4x (the config #1 gate's share).  A kernel defect would put every round far out."""
+    import torch
     from oracle import cnn as ocnn
     from mplc.engine import CoalitionEngine
     eng = CoalitionEngine.for_scenario(mnist10, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
-    coals = [(0,), (4,), (9,), (1, 2), (3, 8), (5, 7), (0, 6, 9), (1, 4, 5, 8)]
-    dev = eng.evaluate(coals, epoch_count=2)
     ds = mnist10.dataset
     data = ocnn.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
     prow = [p.train_idx for p in mnist10.partners_list]
     bs = [p.batch_size for p in mnist10.partners_list]
-    ref = np.array([ocnn.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=2, M=20)[0] for k in coals])
-    diff = dev - ref
-    print(list(zip(coals, dev.tolist(), ref.tolist())))
-    assert abs(np.mean(diff)) <= 0.01, (dev, ref)
-    assert np.max(np.abs(diff)) <= 0.02, (dev, ref)
+    M = mnist10.minibatch_count
+    threads0 = torch.get_num_threads()
+    coal = (2, 9)
+    st = eng.trainer.prepare([coal], 1)
+    errs = []
+    for m in range(M):
+        start = st.glob[0].cpu().numpy().copy()
+        for s in range(m * st.round_len, (m + 1) * st.round_len):
+            st.step(s)
+        st.aggregate(epoch_end=(m == M - 1))
+        torch.cuda.synchronize()
+        dev = st.glob[0].cpu().numpy()
+        glob = ocnn.unpack(start)
+        g64 = ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=M, e=0, m=m, precise=True)
+        g32s = []
+        for th in sorted({1, 2, 3, 8, threads0}):
+            torch.set_num_threads(th)
+            g32s.append(ocnn.fedavg_round(data, prow, bs, coal, glob, seed=eng.seed, M=M, e=0, m=m))
+        torch.set_num_threads(threads0)
+        row = {}
+        for name, (off, shape) in ocnn.OFF.items():
+            n = int(np.prod(shape))
+            ref = g64[name].numpy().reshape(-1)
+            upd = np.linalg.norm(ref - start[off:off + n].astype(np.float64))
+            e_dev = np.linalg.norm(dev[off:off + n].astype(np.float64) - ref) / upd
+            e_cpu = max(np.linalg.norm(g[name].numpy().reshape(-1).astype(np.float64) - ref) / upd for g in g32s)
+            row[name] = (float(e_dev), float(e_cpu))
+        errs.append(row)
+    del st
+    report, bad = [], []
+    for name in ocnn.OFF:
+        med_dev = float(np.median([r[name][0] for r in errs]))
+        med_cpu = float(np.median([r[name][1] for r in errs]))
+        report.append((name, med_dev, med_cpu))
+        if not med_dev <= 4 * med_cpu:
+            bad.append(report[-1])
+    outliers = [m for m, r in enumerate(errs) if any(r[k][0] > 4 * r[k][1] for k in r)]
+    report.append(("outlier rounds", outliers))
+    print(report)
+    assert not bad, (bad, report)
+    assert len(outliers) <= 8, report
+
+
+E2_BAND = 0.01  # the per-coalition gates at E=2: the references' range + 1 pt on each side, fixed
+
+
+def e2_band_check(dev, refs, coals):
+    """Each coalition within [min(refs) - 1 pt, max(refs) + 1 pt] (refs: [reference run][coalition]) and the mean
+    signed difference to the references' median within 1 pt."""
+    refs = np.asarray(refs, dtype=np.float64)
+    lo, hi = refs.min(axis=0) - E2_BAND, refs.max(axis=0) + E2_BAND
+    med = np.median(refs, axis=0)
+    print(list(zip(coals, dev.tolist(), refs.min(axis=0).tolist(), refs.max(axis=0).tolist())))
+    assert abs(np.mean(dev - med)) <= 0.01, (dev, med)  # no systematic bias
+    bad = [(k, float(d), float(a), float(b)) for k, d, a, b in zip(coals, dev, lo, hi) if not a <= d <= b]
+    assert not bad, bad
+
+
+def test_config3_e2_accuracies_vs_oracle(mnist10):
+    """The per-coalition accuracy gate of config #3: v(S) at E=2, the bench's config #3 setting,
+    where the models have left the steep first epoch (test_config3_small_coalitions_vs_oracle's docstring), for all
+    ten singletons and the eight pairs of the E=1 test, fixed before any run.  References: the oracle at 1, 2, 3, 4,
+    6, 8, 12 and 16 CPU threads and in fp64 (tests/golden/oracle_spread_config3_e2.json, scripts/oracle_spread.py)
+    and one live run at the box's thread count.  Gate: each coalition within the references' range + 1 pt on each
+    side (fixed: no multiplier), the mean signed difference to their median within 1 pt."""
+    import copy
+    import torch
+    from spread_fixtures import CONFIG3_COALS, load_spread, oracle_values
+    from mplc.engine import CoalitionEngine
+    eng = CoalitionEngine.for_scenario(mnist10, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
+    rec = load_spread("config3_e2", mnist10)
+    coals = [tuple(k) for k in rec["coalitions"]]
+    assert coals == CONFIG3_COALS
+    dev = eng.evaluate(coals, epoch_count=2)
+    sc2 = copy.copy(mnist10)
+    sc2.epoch_count = 2  # the oracle's E (oracle_values reads the scenario's)
+    refs = [rec["fp32"][str(t)] for t in rec["threads"]] + [rec["fp64"]]
+    refs.append(oracle_values(sc2, coals, torch.get_num_threads(), seed=eng.seed))
+    e2_band_check(dev, refs, coals)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -423,20 +503,22 @@ def test_config4_learned_accuracies_vs_oracle(cifar20):
     fixed before looking at any result.  At E=1 these models sit in a bimodal "aha" regime (0.25-0.6, the same
     coalitions reach 0.97-0.99 at E=2: scripts/probe_cifar_signal.py in the build container), where a statement of
     +-1 pt says little; at E=2 they classify 97-99 % of the test set, so a point is a third of the error.
-    Gate: mean signed difference <= 1 pt, each coalition <= 2 pt (the oracle sequential, at the box's threads)."""
-    from oracle import cifar_cnn as occ
+    Gate (tightened from 2 pt per coalition): each coalition within the oracle's range over 1, 2,
+    3, 4, 6, 8, 12 and 16 CPU threads (tests/golden/oracle_spread_config4_e2.json; the CIFAR oracle has no fp64 mode)
+    and one live run at the box's thread count, + 1 pt on each side, fixed; mean signed difference to their median
+    within 1 pt."""
+    import copy
+    import torch
+    from spread_fixtures import CONFIG4_E2_COALS, load_spread, oracle_values
     from mplc.engine import CoalitionEngine
     eng = CoalitionEngine.for_scenario(cifar20, memory_budget_bytes=16 << 30, eval_budget_bytes=2 << 30)
-    coals = [(2, 9, 14), (0, 7, 11, 16), (1, 4, 6, 11, 15, 19), (3, 5, 8, 10, 12), (2, 9, 14, 17),
-             (0, 3, 5, 8, 10, 12, 13, 18), (6, 13, 17), (1, 7, 15, 18)]
+    rec = load_spread("config4_e2", cifar20)
+    coals = [tuple(k) for k in rec["coalitions"]]
+    assert coals == CONFIG4_E2_COALS
     dev = eng.evaluate(coals, epoch_count=2)
-    ds = cifar20.dataset
-    data = occ.Data(ds.x_train, ds.y_train, ds.x_val, ds.y_val, ds.x_test, ds.y_test)
-    prow = [p.train_idx for p in cifar20.partners_list]
-    bs = [p.batch_size for p in cifar20.partners_list]
-    ref = np.array([occ.coalition_value(data, prow, bs, k, seed=eng.seed, epochs=2, M=20)[0] for k in coals])
-    diff = dev - ref
-    print(list(zip(coals, dev.tolist(), ref.tolist())))
-    assert np.min(ref) >= 0.5 and np.min(dev) >= 0.5, (dev, ref)  # the learned regime
-    assert abs(np.mean(diff)) <= 0.01, (dev, ref)
-    assert np.max(np.abs(diff)) <= 0.02, (dev, ref)
+    sc2 = copy.copy(cifar20)
+    sc2.epoch_count = 2
+    refs = [rec["fp32"][str(t)] for t in rec["threads"]]
+    refs.append(oracle_values(sc2, coals, torch.get_num_threads(), seed=eng.seed))
+    assert np.min(refs) >= 0.5 and np.min(dev) >= 0.5, (dev, refs)  # the learned regime
+    e2_band_check(dev, refs, coals)
