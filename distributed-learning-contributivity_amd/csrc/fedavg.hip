@@ -24,7 +24,7 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
                                                      const int32_t* __restrict__ first, const double* __restrict__ w,
                                                      const double* __restrict__ scale, int64_t n_param,
                                                      float* __restrict__ out, int64_t out_stride, int broadcast,
-                                                     int64_t skip_lo, int64_t skip_hi, int vec4) {
+                                                     int64_t skip_lo, int64_t skip_hi, int vec4, int skip_avg) {
   const int c = blockIdx.y;
   const int r0 = first[c];
   const int r1 = first[c + 1];
@@ -32,8 +32,11 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
   const int64_t nthreads = (int64_t)gridDim.x * TPB;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (vec4) {
-    const int64_t n4 = n_param >> 2;
-    for (int64_t k = t; k < n4; k += nthreads) {
+    // skip_avg: the range [skip_lo, skip_hi) is not visited at all (the element index jumps over it)
+    const int64_t lo4 = skip_lo >> 2, gap4 = skip_avg ? (skip_hi - skip_lo) >> 2 : 0;
+    const int64_t n4 = (n_param >> 2) - gap4;
+    for (int64_t kk = t; kk < n4; kk += nthreads) {
+      const int64_t k = kk < lo4 ? kk : kk + gap4;
       const float4 a = reinterpret_cast<const float4*>(x + (int64_t)r0 * x_stride)[k];
       const double w0 = w[r0];
       double s0 = (double)a.x * w0, s1 = (double)a.y * w0, s2 = (double)a.z * w0, s3 = (double)a.w * w0;
@@ -51,7 +54,9 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
         for (int r = r0; r < r1; ++r) reinterpret_cast<float4*>(x + (int64_t)r * x_stride)[k] = res;
     }
   } else {
-    for (int64_t k = t; k < n_param; k += nthreads) {
+    const int64_t gap = skip_avg ? skip_hi - skip_lo : 0;
+    for (int64_t kk = t; kk < n_param - gap; kk += nthreads) {
+      const int64_t k = kk < skip_lo ? kk : kk + gap;
       double s = (double)x[(int64_t)r0 * x_stride + k] * w[r0];
       for (int r = r0 + 1; r < r1; ++r) s = s + (double)x[(int64_t)r * x_stride + k] * w[r];
       const float res = (float)(s / scl);
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(TPB) void fedavg_kernel(float* __restrict__ x, int6
 namespace {
 int fedavg_launch(float* x, int64_t x_stride, const int32_t* first, const double* w, const double* scale,
                   int n_coalitions, int64_t n_param, float* out, int64_t out_stride, int broadcast, int64_t skip_lo,
-                  int64_t skip_hi, void* stream) {
+                  int64_t skip_hi, void* stream, int skip_avg = 0) {
   if (x == nullptr || first == nullptr || w == nullptr || scale == nullptr) return MPLC_E_ARG;
   if (n_coalitions < 1 || n_coalitions > 65535 || n_param < 1 || x_stride < n_param) return MPLC_E_ARG;
   if (out == nullptr && !broadcast) return MPLC_E_ARG;
@@ -75,14 +80,14 @@ int fedavg_launch(float* x, int64_t x_stride, const int32_t* first, const double
   if (skip_lo < 0 || skip_hi < skip_lo || skip_hi > n_param) return MPLC_E_ARG;
   const bool vec4 = ((skip_lo | skip_hi) & 3) == 0 && ((n_param & 3) == 0) && ((x_stride & 3) == 0) && (((uintptr_t)x & 15) == 0) &&
                     (out == nullptr || (((out_stride & 3) == 0) && (((uintptr_t)out & 15) == 0)));
-  const int64_t work = vec4 ? (n_param >> 2) : n_param;
+  const int64_t work = (vec4 ? (n_param >> 2) : n_param) - (skip_avg ? (vec4 ? (skip_hi - skip_lo) >> 2 : skip_hi - skip_lo) : 0);
   int64_t bx = (work + TPB - 1) / TPB;
   // enough blocks to fill 256 CUs across all coalitions, grid-stride the rest
   const int64_t cap = (2048 + n_coalitions - 1) / n_coalitions;
   if (bx > cap) bx = cap < 1 ? 1 : cap;
   dim3 grid((unsigned)bx, (unsigned)n_coalitions);
   fedavg_kernel<<<grid, TPB, 0, (hipStream_t)stream>>>(x, x_stride, first, w, scale, n_param, out, out_stride,
-                                                       broadcast, skip_lo, skip_hi, vec4 ? 1 : 0);
+                                                       broadcast, skip_lo, skip_hi, vec4 ? 1 : 0, skip_avg);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? MPLC_OK : (int)e;
 }
@@ -100,4 +105,12 @@ extern "C" int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, cons
   if (out == nullptr) return MPLC_E_ARG;  // the skipped range's only copy is the coalition row
   return fedavg_launch(x, x_stride, first, w, scale, n_coalitions, n_param, out, out_stride, 1, skip_lo, skip_hi,
                        stream);
+}
+
+extern "C" int mplc_fedavg_aggregate_skip(float* x, int64_t x_stride, const int32_t* first, const double* w,
+                                          const double* scale, int n_coalitions, int64_t n_param, float* out,
+                                          int64_t out_stride, int64_t skip_lo, int64_t skip_hi, void* stream) {
+  if (out == nullptr || skip_hi <= skip_lo) return MPLC_E_ARG;
+  return fedavg_launch(x, x_stride, first, w, scale, n_coalitions, n_param, out, out_stride, 1, skip_lo, skip_hi,
+                       stream, 1);
 }

@@ -579,18 +579,14 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ H, 
 constexpr int D1_ROWS = 32;    // W3 rows per block (8 threads per row)
 constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
-__global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
-    const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
+// One replica's pass over one 32-row slice of W3 (the body of dense1_bwd_adam_kernel, shared with the fused
+// averaging kernel below): dp rows written, W3's moments read / written by the optimizer step, b3 updated by the
+// slice-0 block; the updated slice is returned in w (lane's fvec4 chunks c8 + 8 i) - the caller stores it.
+__device__ __forceinline__ void dense1_replica_slice(
+    int r, int k0, int count, const float* __restrict__ Pool, const float* __restrict__ dH,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
-    float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
-  __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
-  __shared__ float p_s[D1_SCHUNK * D1_ROWS];
-  const int64_t lb = xcd_block();  // logical block (slice, r), replica-major: dh and p stay in one L2
-  const int r = (int)(lb / gridDim.x);
-  const int k0 = (int)(lb % gridDim.x) * D1_ROWS;
-  const int count = cnt[r];
-  if (count == 0) return;
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps, fvec4* dh_s, float* p_s, fvec4 (&w)[4]) {
   const int tid = threadIdx.x;
   const int rowl = tid >> 3;
   // the 8 threads of a row own interleaved fvec4 chunks q = c8 + 8*i (columns 4q..4q+3): each global
@@ -602,7 +598,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   // are read and written as usual; an optimizer's last step writes neither (the next step starts fresh)
   const bool fresh = cfg.reset, second = (cfg.t == 2);
   const int64_t roff = (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + rowl) * HID;
-  fvec4* W = reinterpret_cast<fvec4*>(params + roff) + c8;
+  const fvec4* W = reinterpret_cast<const fvec4*>(params + roff) + c8;
   // a round's first step reads W3 from the coalition row (the aggregation did not broadcast it)
   const int gsrc = w3src ? w3src[r] : -1;
   const fvec4* Wsrc = gsrc >= 0 ? reinterpret_cast<const fvec4*>(glob + roff + (int64_t)(gsrc - r) * stride) + c8 : W;
@@ -610,7 +606,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   fvec4* Vr = reinterpret_cast<fvec4*>(adam_v + roff) + c8;
   const fvec4 z4 = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
   // every HBM read of the pass is issued up front; the moments land while the gradient is accumulated
-  fvec4 w[4], g[4], mv[4], vv[4];
+  fvec4 g[4], mv[4], vv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     w[i] = Wsrc[8 * i];
@@ -685,7 +681,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
       mv[i][q] = m1;
       vv[i][q] = v1;
     }
-    W[8 * i] = pw;
+    w[i] = pw;
     if (!cfg.last) {
       if (fresh) {
         __builtin_nontemporal_store(g[i], Mr + 8 * i);
@@ -702,6 +698,78 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
     const int64_t o = (int64_t)r * stride + OFF_B3 + tid;
     adam_apply(params[o], adam_m[o], adam_v[o], gb, cfg);
   }
+}
+
+__global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
+    const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
+    const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
+    float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps, const int32_t* __restrict__ avg_rep) {
+  __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
+  __shared__ float p_s[D1_SCHUNK * D1_ROWS];
+  const int64_t lb = xcd_block();  // logical block (slice, r), replica-major: dh and p stay in one L2
+  const int r = (int)(lb / gridDim.x);
+  const int k0 = (int)(lb % gridDim.x) * D1_ROWS;
+  const int count = cnt[r];
+  if (count == 0) return;
+  if (avg_rep && avg_rep[r]) return;  // this step's pass of r belongs to dense1_bwd_adam_avg_kernel
+  fvec4 w[4];
+  dense1_replica_slice(r, k0, count, Pool, dH, adam_t, bmax, params, adam_m, adam_v, stride, glob, w3src, dPool, lr,
+                       b1, b2, eps, dh_s, p_s, w);
+  fvec4* W = reinterpret_cast<fvec4*>(params + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + (threadIdx.x >> 3)) * HID) +
+             (threadIdx.x & 7);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) W[8 * i] = w[i];
+}
+
+// The last step of a FedAvg round with the coalition's W3 average fused in.
+// Block = (32-row slice, fused coalition c): the coalition's replicas in order, each the pass of
+// dense1_bwd_adam_kernel (the same code: dp rows, b3), and instead of storing the replica's updated slice, its
+// np.average term: s = x_0 w_0, then s = s + x_r w_r in replica order in fp64, one division by the weights' sum,
+// one rounding to fp32 - mplc_fedavg_aggregate's arithmetic (no contraction), written to the coalition row.  The
+// replicas' own W3 rows are neither written here nor read by the aggregation (mplc_fedavg_aggregate_skip leaves
+// W3 out), and the next round's first step reads W3 from the coalition row (w3src): every replica W3 store of the
+// round's last step and the aggregation's W3 reads disappear.  A member without a step this time (it finished
+// its round's fit earlier: fewer rows) enters with its own row, as the aggregation would read it.
+__global__ __launch_bounds__(256) void dense1_bwd_adam_avg_kernel(
+    const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
+    const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
+    float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps, const int32_t* __restrict__ avg_first,
+    const double* __restrict__ avg_w, const double* __restrict__ avg_scale, const int32_t* __restrict__ avg_glob,
+    float* __restrict__ avg_out) {
+#pragma clang fp contract(off)
+  __shared__ fvec4 dh_s[D1_SCHUNK * (HID / 4)];
+  __shared__ float p_s[D1_SCHUNK * D1_ROWS];
+  const int64_t lb = xcd_block();  // logical block (slice, coalition), coalition-major
+  const int c = (int)(lb / gridDim.x);
+  const int k0 = (int)(lb % gridDim.x) * D1_ROWS;
+  const int r0 = avg_first[2 * c], r1 = avg_first[2 * c + 1];
+  const int64_t soff = OFF_W3 + (int64_t)(k0 + (threadIdx.x >> 3)) * HID;
+  const int c8 = threadIdx.x & 7;
+  double s[4][4];
+  for (int r = r0; r < r1; ++r) {
+    const int count = cnt[r];  // block-uniform
+    fvec4 w[4];
+    if (count == 0) {
+      const fvec4* W = reinterpret_cast<const fvec4*>(params + (int64_t)r * stride + soff) + c8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = W[8 * i];
+    } else {
+      dense1_replica_slice(r, k0, count, Pool, dH, adam_t, bmax, params, adam_m, adam_v, stride, glob, w3src, dPool,
+                           lr, b1, b2, eps, dh_s, p_s, w);
+    }
+    const double wr = avg_w[r];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[i][q] = (r == r0) ? (double)w[i][q] * wr : s[i][q] + (double)w[i][q] * wr;
+  }
+  const double scl = avg_scale[c];
+  fvec4* O = reinterpret_cast<fvec4*>(avg_out + (int64_t)avg_glob[c] * stride + soff) + c8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    O[8 * i] = fvec4{(float)(s[i][0] / scl), (float)(s[i][1] / scl), (float)(s[i][2] / scl), (float)(s[i][3] / scl)};
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -732,7 +800,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
-    float* __restrict__ dPool, float lr, float b1, float b2, float eps) {
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps, const int32_t* __restrict__ avg_rep) {
   __shared__ float smem[D1M_LDS];
   float* const dh_s = smem;                            // [sample][D1M_DHS]
   float* const p_s = smem + D1M_SCHUNK * D1M_DHS;     // [sample][D1M_PS]
@@ -741,6 +809,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int k0 = (int)(lb % gridDim.x) * D1M_ROWS;
   const int count = cnt[r];
   if (count == 0) return;
+  if (avg_rep && avg_rep[r]) return;  // this step's pass of r belongs to dense1_bwd_adam_avg_kernel
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int tl = lane & 15, kq = lane >> 4;
@@ -1412,6 +1481,9 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
   if (t->minibatch_count < 1 || t->round_len < 1 || t->epochs < 1) return MPLC_E_ARG;
   if (t->glob && (!t->rep_glob || !t->w3src)) return MPLC_E_ARG;
   if (t->phases & ~(MPLC_PHASE_FRONT | MPLC_PHASE_DENSE | MPLC_PHASE_BACK)) return MPLC_E_ARG;
+  if (t->avg_n < 0 || t->avg_n > 65535 ||
+      (t->avg_n > 0 && (!t->avg_first || !t->avg_w || !t->avg_scale || !t->avg_glob || !t->avg_out || !t->avg_rep)))
+    return MPLC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int R = t->n_rep, B = t->bmax;
   const int64_t S = MPLC_CNN_STRIDE;
@@ -1440,17 +1512,22 @@ int mplc_cnn_train_step(const mplc_cnn_train_t* t, void* stream) {
                                 S, t->dhidden, t->lr, t->beta1, t->beta2, t->eps, t->hstats);
   PROF_END(3);
   PROF_BEGIN(4);
+  const int32_t* avg_rep = t->avg_n > 0 ? t->avg_rep : nullptr;
 #if MPLC_D1_MFMA
   dense1_bwd_adam_mfma_kernel<<<dim3(FEAT / D1M_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                        t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                        w3src, t->dpooled,
-                                                                       t->lr, t->beta1, t->beta2, t->eps);
+                                                                       t->lr, t->beta1, t->beta2, t->eps, avg_rep);
 #else
   dense1_bwd_adam_kernel<<<dim3(FEAT / D1_ROWS, R), 256, 0, s>>>(t->pooled, t->dhidden, t->cnt, t->adam_t, B,
                                                                   t->params, t->adam_m, t->adam_v, S, t->glob,
                                                                   w3src, t->dpooled,
-                                                                  t->lr, t->beta1, t->beta2, t->eps);
+                                                                  t->lr, t->beta1, t->beta2, t->eps, avg_rep);
 #endif
+  if (t->avg_n > 0)  // the round's last step of the fused coalitions: their W3 passes and the W3 average
+    dense1_bwd_adam_avg_kernel<<<dim3(FEAT / D1_ROWS, t->avg_n), 256, 0, s>>>(
+        t->pooled, t->dhidden, t->cnt, t->adam_t, B, t->params, t->adam_m, t->adam_v, S, t->glob, w3src, t->dpooled,
+        t->lr, t->beta1, t->beta2, t->eps, t->avg_first, t->avg_w, t->avg_scale, t->avg_glob, t->avg_out);
   PROF_END(4);
   }
   if (ph & MPLC_PHASE_BACK) {

@@ -27,6 +27,8 @@ SIGNATURES = {
                                       c_int64, c_int, c_void_p]),
     "mplc_fedavg_aggregate_bcast_skip": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int64,
                                                  c_void_p, c_int64, c_int64, c_int64, c_void_p]),
+    "mplc_fedavg_aggregate_skip": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p,
+                                           c_int64, c_int64, c_int64, c_void_p]),
     # Monte-Carlo Shapley permutation walks over a dense table (csrc/mc_shapley.hip)
     "mplc_tmc_walk": (c_int, [c_void_p, c_int, c_void_p, c_int, ctypes.c_double, ctypes.c_double, c_int, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -60,7 +62,7 @@ SIGNATURES = {
                                c_void_p]),
 }
 
-ABI_VERSION = 3  # include/mplc_hip.h MPLC_ABI_VERSION
+ABI_VERSION = 4  # include/mplc_hip.h MPLC_ABI_VERSION
 
 
 def check_layout(query, expected, what):

@@ -78,7 +78,10 @@ class TrainT(ctypes.Structure):
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("prof_kernel", ctypes.c_int32), ("phases", ctypes.c_int32),
                 ("prof_begin", ctypes.c_void_p), ("prof_end", ctypes.c_void_p), ("hstats", ctypes.c_void_p),
-                ("glob", ctypes.c_void_p), ("rep_glob", ctypes.c_void_p), ("w3src", ctypes.c_void_p)]
+                ("glob", ctypes.c_void_p), ("rep_glob", ctypes.c_void_p), ("w3src", ctypes.c_void_p),
+                ("avg_n", ctypes.c_int32), ("pad1", ctypes.c_int32), ("avg_first", ctypes.c_void_p),
+                ("avg_w", ctypes.c_void_p), ("avg_scale", ctypes.c_void_p), ("avg_glob", ctypes.c_void_p),
+                ("avg_out", ctypes.c_void_p), ("avg_rep", ctypes.c_void_p)]
 
 KERNEL_IDS = {"conv_fwd": 1, "dense_fwd": 2, "head": 3, "dense1_bwd_adam": 4, "conv_bwd_data": 5, "conv_wgrad": 6,
               "adam_small": 7}
@@ -211,6 +214,9 @@ class MnistModel:
     # FedAvg aggregation leaves W3 (98 % of the parameters) out of the broadcast: a round's first step reads
     # it from the coalition row (mplc_cnn_train_t.glob, mplc_fedavg_aggregate_bcast_skip)
     BCAST_SKIP = (KERAS_LAYERS[4][0], KERAS_LAYERS[5][0])
+    # ... and the round's last step can average it in its dense pass (mplc_cnn_train_t.avg_*, ABI 4): the
+    # aggregation then skips that range altogether (mplc_fedavg_aggregate_skip)
+    FUSE_AVG = True
 
     def __init__(self):
         _bind()
@@ -273,9 +279,12 @@ class MnistModel:
             st.t.prof_begin, st.t.prof_end = ev0, ev1
         else:
             st.t.prof_kernel, st.t.prof_begin, st.t.prof_end = 0, None, None
+        fused = st.fused_step(s)  # the round's last step: W3's average in the dense pass
+        st.t.avg_n = st.avg["n"] if fused else 0
         _native.check(self.lib.mplc_cnn_train_step(ctypes.byref(st.t), st.stream), "mplc_cnn_train_step")
         if prof is not None and prof.want_stash:
-            prof.stash_step(st.ws["cnt"], st.ws["adam_t"], st.ws["w3src"])
+            prof.stash_step(st.ws["cnt"], st.ws["adam_t"], st.ws["w3src"],
+                            st.avg["rep"] if fused else st.avg_none)
 
     @staticmethod
     def algorithmic_units(stash):
@@ -296,7 +305,9 @@ class MnistModel:
         # a job into several (the per-step copies then have different lengths)
         w3 = float(FEAT * HID * 4)
         samples = d1_bytes = df_bytes = 0.0
-        for cnt, at, src in stash:
+        for rec in stash:
+            cnt, at, src = rec[:3]
+            fused = rec[3] if len(rec) > 3 else torch.zeros_like(cnt)  # 1 + fused coalition index, or 0
             cnt = cnt.to(torch.float64)
             shared = src >= 0
             # distinct coalition rows read by this step's first-step replicas
@@ -307,10 +318,15 @@ class MnistModel:
             mom_rd = torch.where(t == 1, 0.0, torch.where(t == 2, 1.0, 2.0)).to(torch.float64)
             mom_wr = torch.where(last, 0.0, torch.where(t == 1, 1.0, 2.0)).to(torch.float64)
             own = (~shared).to(torch.float64)  # replicas reading W3 from their own row
-            d1 = act * (w3 * (1.0 + own + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
+            # the W3 store: the replica's own row, or for a fused coalition (the round's last step) one coalition
+            # row per coalition, and its members idle this step read their final rows into the average
+            wr = (fused == 0).to(torch.float64)
+            idle_fused = float(((fused > 0) & (cnt == 0)).sum().item())
+            n_avg_rows = float(torch.unique(fused[fused > 0]).numel())
+            d1 = act * (w3 * (wr + own + mom_rd + mom_wr) + cnt * float(2 * FEAT * 4 + HID * 4))
             df = act * (w3 * own + cnt * float(FEAT * 4 + HID * 4))
             samples += float(cnt.sum().item())
-            d1_bytes += float(d1.sum().item()) + n_shared_rows * w3
+            d1_bytes += float(d1.sum().item()) + (n_shared_rows + n_avg_rows + idle_fused) * w3
             df_bytes += float(df.sum().item()) + n_shared_rows * w3
         return {"samples": samples, "dense1_bwd_adam_bytes": d1_bytes, "dense_fwd_bytes": df_bytes}
 
@@ -448,6 +464,8 @@ class TrainBatch:
             self.t.hstats = self.hstats.data_ptr()
         self.stopped = np.zeros(C, dtype=bool)
         self.kind_host = self.rep_arr["kind"].copy()
+        self.avg = {"n": 0}
+        self.avg_none = torch.zeros(R, **i32)  # the stash's "no fused coalition" record (bench accounting)
         self.run_args = self.make_runs()
 
     def make_runs(self):
@@ -500,7 +518,51 @@ class TrainBatch:
                              for ci in run for p in self.coalitions[ci] for m in range(self.eng.minibatch_count))
             args.append((self.coal_first[run[0]], run[0], len(run), f_dev[fo:fo + fn], x_dev[xo:xo + wn],
                          x_dev[xo + wn:xo + wn + sn], full_bcast))
-        return args
+        return self._fuse_runs(args)
+
+    def _fuse_runs(self, args):
+        """Runs whose W3 average the round's last step computes in its dense pass (mplc_cnn_train_t.avg_*, ABI 4):
+        FedAvg runs that broadcast with W3 skipped, for a model with the fused kernel, without history recording
+        (the partners' val evaluations read the replicas' own W3 rows, which a fused step does not write).  Each
+        run's tuple gains a flag; the step's tables cover all fused runs of the batch."""
+        import torch
+        eng = self.eng
+        ok = (getattr(self.model, "FUSE_AVG", False) and not self.seq_mode and eng.bcast_skip and not self.record
+              and getattr(eng, "fuse_avg", True))
+        out, first, rep_w, scale, glob_row = [], [], np.zeros(self.R), [], []
+        rep = np.zeros(self.R, dtype=np.int32)
+        sizes = eng.partner_sizes
+        for (r0, c0, nc, f, w, sc, full_bcast) in args:
+            fuse = bool(ok and not full_bcast)
+            out.append((r0, c0, nc, f, w, sc, full_bcast, fuse))
+            if not fuse:
+                continue
+            for ci in range(c0, c0 + nc):
+                b, e = self.coal_first[ci], self.coal_first[ci + 1]
+                ww, scl = aggregation_weights([sizes[p] for p in self.coalitions[ci]], eng.aggregation)
+                rep_w[b:e] = ww
+                rep[b:e] = len(scale) + 1
+                first.extend([b, e])
+                scale.append(scl)
+                glob_row.append(ci)
+        if not scale:
+            self.avg = {"n": 0}
+            return out
+        dev = self.dev
+        self.avg = {"n": len(scale), "first": torch.tensor(first, **self.i32),
+                    "w": torch.from_numpy(rep_w).to(dev), "scale": torch.tensor(scale, dtype=torch.float64, device=dev),
+                    "glob": torch.tensor(glob_row, **self.i32), "rep": torch.from_numpy(rep).to(dev)}
+        t = self.t
+        t.avg_first, t.avg_w, t.avg_scale = (self.avg["first"].data_ptr(), self.avg["w"].data_ptr(),
+                                             self.avg["scale"].data_ptr())
+        t.avg_glob, t.avg_out, t.avg_rep = (self.avg["glob"].data_ptr(), self.glob.data_ptr(),
+                                            self.avg["rep"].data_ptr())
+        return out
+
+    def fused_step(self, s):
+        """Step s is the last step of a FedAvg round and the batch has fused runs: the step averages their W3."""
+        return (self.avg["n"] > 0 and self.fed_steps > 0 and s < self.fed_steps
+                and (s + 1) % self.round_len == 0)
 
     def step(self, s):
         self.model.step(self, s, self.eng.profiler)
@@ -525,12 +587,17 @@ class TrainBatch:
         S, NP = self.model.STRIDE, self.model.NPARAM
         aggregate_now = (not self.seq_mode or self.approach == "seqavg"
                          or (self.approach == "seq-with-final-agg" and epoch_end))
-        for (r0, c0, nc, first, w, sc, full_bcast) in self.run_args:
+        for (r0, c0, nc, first, w, sc, full_bcast, fused) in self.run_args:
             if aggregate_now:
                 x = self.params[r0:] if not self.seq_mode else self.snap[self.snap_row(c0):]
                 skip = None if (self.seq_mode or full_bcast or not self.eng.bcast_skip) else \
                     getattr(self.model, "BCAST_SKIP", None)
-                if skip is not None:  # the next round's first step reads this range from glob
+                if fused:  # the round's last step wrote W3's average into glob: the other layers only
+                    _native.check(self.lib.mplc_fedavg_aggregate_skip(
+                        _native.ptr(x), S, _native.ptr(first), _native.ptr(w), _native.ptr(sc), nc, NP,
+                        _native.ptr(self.glob[c0:c0 + nc]), S, skip[0], skip[1], self.stream),
+                        "mplc_fedavg_aggregate_skip")
+                elif skip is not None:  # the next round's first step reads this range from glob
                     _native.check(self.lib.mplc_fedavg_aggregate_bcast_skip(
                         _native.ptr(x), S, _native.ptr(first), _native.ptr(w), _native.ptr(sc), nc, NP,
                         _native.ptr(self.glob[c0:c0 + nc]), S, skip[0], skip[1], self.stream),

@@ -104,6 +104,9 @@ class CoalitionEngine:
         # FedAvg rounds leave the large dense layer out of the broadcast (the next round's first step reads it
         # from the coalition row); False broadcasts every layer (the plain copy-back, for A/B tests)
         self.bcast_skip = True
+        # the round's last step averages W3 in its dense pass (MNIST; ABI 4): MPLC_FUSE_AVG=0 keeps the
+        # separate aggregation of every layer (A/B and bit-identity tests)
+        self.fuse_avg = os.environ.get("MPLC_FUSE_AVG", "1") != "0"
         self.stats = {"coalitions": 0, "batches": 0, "replicas": 0, "samples": 0}
 
     # --------------------------------------------------------------------------------------------

@@ -33,8 +33,10 @@ extern "C" {
 
 /* Version / capability probe: returns MPLC_ABI_VERSION.  Version 2: the CIFAR10 Winograd weight workspace
  * (MPLC_CIFAR_WT 114688) and the layout queries mplc_cnn_layout / mplc_cifar_layout.  Version 3: the CIFAR10
- * pooled-gradient slots dz4 / dz2 at their pooled sizes (MPLC_CIFAR_DZ4 2304, MPLC_CIFAR_DZ2 7200). */
-#define MPLC_ABI_VERSION 3
+ * pooled-gradient slots dz4 / dz2 at their pooled sizes (MPLC_CIFAR_DZ4 2304, MPLC_CIFAR_DZ2 7200).  Version 4: the
+ * round's last step may fuse W3's FedAvg average into the MNIST dense pass (mplc_cnn_train_t.avg_*) and
+ * mplc_fedavg_aggregate_skip aggregates the other layers. */
+#define MPLC_ABI_VERSION 4
 int mplc_abi_version(void);
 
 /* ------------------------------------------------------------------------------------------------
@@ -90,6 +92,14 @@ int mplc_fedavg_aggregate(float* x, int64_t x_stride, const int32_t* first, cons
 int mplc_fedavg_aggregate_bcast_skip(float* x, int64_t x_stride, const int32_t* first, const double* w,
                                      const double* scale, int n_coalitions, int64_t n_param, float* out,
                                      int64_t out_stride, int64_t skip_lo, int64_t skip_hi, void* stream);
+
+/* As mplc_fedavg_aggregate_bcast_skip, except that parameters [skip_lo, skip_hi) are neither averaged nor
+ * written anywhere: out[c]'s range is left as it is (ABI 4: the MNIST trainer's W3, whose average the round's
+ * last step already wrote there - mplc_cnn_train_t.avg_*).  Every other parameter is averaged into out[c] and
+ * broadcast to the replica rows, bit-identical to mplc_fedavg_aggregate. */
+int mplc_fedavg_aggregate_skip(float* x, int64_t x_stride, const int32_t* first, const double* w, const double* scale,
+                               int n_coalitions, int64_t n_param, float* out, int64_t out_stride, int64_t skip_lo,
+                               int64_t skip_hi, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Batched FedAvg logistic regression (Titanic model, BASELINE config #2), all coalitions at once: per FedAvg

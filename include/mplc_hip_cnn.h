@@ -142,6 +142,21 @@ typedef struct {
   const float* glob;      /* [n_coalitions][MPLC_CNN_STRIDE] coalition models                    */
   const int32_t* rep_glob;  /* [n_rep] replica -> its coalition's row of glob                 */
   int32_t* w3src;         /* [n_rep] workspace: glob row W3 is read from this step, or -1      */
+  /* optional (ABI 4; avg_n = 0: off): the last step of a FedAvg round with W3's data-volume average fused into
+   * the dense pass (replaces the W3 part of mplc_fedavg_aggregate, mplc/mpl_utils.py:90-115).  For each of the
+   * avg_n coalitions (replicas avg_first[2c] .. avg_first[2c + 1] - 1, contiguous) the step computes every member's
+   * updated W3 as usual and writes np.average of them - fp64 products x * avg_w[r] added in replica order, divided
+   * by avg_scale[c], rounded once - into row avg_glob[c] of avg_out, not into the replicas' rows; the host then
+   * aggregates the other layers with mplc_fedavg_aggregate_skip over [MPLC_CNN_OFF_W3, MPLC_CNN_OFF_B3).
+   * avg_rep[r] != 0 marks the replicas of those coalitions.  Only a round's last step may carry it. */
+  int32_t avg_n;
+  int32_t pad1;
+  const int32_t* avg_first;  /* [2 avg_n] the coalitions' replica ranges (begin, end)           */
+  const double* avg_w;       /* [n_rep] the replica's aggregation weight (data volume / uniform)  */
+  const double* avg_scale;   /* [avg_n] the coalition's sum of weights                          */
+  const int32_t* avg_glob;   /* [avg_n] the coalition's row of avg_out                          */
+  float* avg_out;            /* coalition rows (the same array as glob)                         */
+  const int32_t* avg_rep;    /* [n_rep]                                                         */
 } mplc_cnn_train_t;
 
 /* Parameter row stride in floats (== MPLC_CNN_STRIDE). */

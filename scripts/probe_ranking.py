@@ -30,20 +30,22 @@ GEO = [0.02, 0.03, 0.04, 0.06, 0.08, 0.10, 0.12, 0.15, 0.18, 0.22]  # np.sum == 
 WIDE = [0.04, 0.05, 0.06, 0.08, 0.09, 0.10, 0.12, 0.13, 0.15, 0.18]  # np.sum == 1.0 exactly
 
 
+RAISED = [0.04, 0.05, 0.06, 0.07, 0.08, 0.10, 0.12, 0.14, 0.16, 0.18]  # np.sum == 1.0 exactly
+
+
 def candidates():
     """name -> (amounts, signal, dataset_proportion, n_test, E, M, G, split): every partner with at least M * G rows
-    (batch size >= 1), enough optimizer steps per epoch (M x G) to learn.  Round 6's first two grids (random split,
-    GEO amounts, signal 0.1 / 0.2, E 1 .. 4): no candidate kept one ranking over 3-4 seeds (profiles/
-    r06_probe_ranking.log): random partitions of template data differ only in volume, and small-data training is
-    chaotic.  The stratified split (mplc/scenario.py:571-681: rows sorted by label, so a partner holds a run of
-    classes) makes a partner's value the classes it brings, which a fork in training does not change."""
+    (batch size >= 1), enough optimizer steps per epoch (M x G) to learn.  Grids 1-3 (profiles/r06_probe_ranking_*):
+    random partitions of class-template data at signal 0.2 - 0.3 learn to v(N) ~ 0.9 - 1.0 with a partner ranking
+    that survives ~1-ulp perturbations of the data, except where the two smallest partners contribute ~0 and tie; the
+    stratified split (a partner holds a run of classes) does not learn at these sizes.  Grid 4: the random split with
+    a raised minimum amount and fewer, larger steps (fewer rounds: what the CPU oracle's sweep pays for)."""
     out = {}
-    for split in ("stratified", "random"):
-        for amounts, aname in ((GEO, "geo"), (WIDE, "wide")):
-            for signal in (0.2, 0.3):
-                for prop, M, G, E in ((0.05, 5, 8, 4), (0.1, 10, 8, 2), (0.1, 10, 8, 4)):
-                    out[f"{split[:5]}_{aname}_s{signal}_p{prop}_m{M}_g{G}_e{E}"] = (amounts, signal, prop, 1000, E, M,
-                                                                                    G, split)
+    for amounts, aname in ((RAISED, "raised"), (GEO, "geo")):
+        for signal in (0.2, 0.25):
+            for prop, M, G, E in ((0.1, 10, 8, 4), (0.1, 2, 16, 4), (0.1, 1, 32, 4), (0.1, 2, 16, 6)):
+                out[f"rando_{aname}_s{signal}_p{prop}_m{M}_g{G}_e{E}"] = (amounts, signal, prop, 1000, E, M, G,
+                                                                          "random")
     return out
 
 
@@ -100,11 +102,19 @@ def main():
         m = svs.mean(0)
         gaps = np.diff(np.sort(m))
         std = svs.std(0).max()
+        o = np.argsort(m)
+        sd = svs.std(0)
+        z = [float((m[o[i + 1]] - m[o[i]]) / max(np.hypot(sd[o[i]], sd[o[i + 1]]), 1e-9)) for i in range(len(o) - 1)]
         samp_epochs = sum(sum(sizes[p] for p in c) for c in coals) * E
         cost_tflop = (samp_epochs * 71.565312e6 + len(coals) * n_test * 23.984896e6) / 1e12
         rec = {"sizes": sizes, "batch_sizes": bsz, "v_all": vn, "sv_seed0": svs[0].round(4).tolist(),
                "sv_mean": m.round(4).tolist(), "sv_std_max": float(std), "min_gap": float(gaps.min()),
                "gap_over_std": float(gaps.min() / max(std, 1e-9)), "ranking_same_all_seeds": same,
+               "min_gap_z": float(min(z)), "gap_z": [round(v, 2) for v in z],
+               # optimizer steps of the sequential sweep (each partner is in 512 of the 1023 coalitions): what the
+               # CPU oracle pays ~20-40 ms each for at these batch sizes
+               "sweep_steps": int(512 * E * M * sum(-(-(len(p.train_idx) // M + 1) // max(1, p.batch_size))
+                                                    for p in sc.partners_list)),
                "singletons_seed0": single, "oracle_cost_tflop": round(cost_tflop, 1), "wall_s": round(time.time() - t0, 1)}
         out[name] = rec
         print(name, json.dumps(rec), flush=True)

@@ -165,8 +165,15 @@ def test_one_adam_step_matches_keras_adam(scenario, engine, odata):
 
 
 def test_fedavg_aggregation_inside_training_is_np_average(scenario, engine):
+    """The separate aggregation (fuse_avg off: every layer averaged by mplc_fedavg_aggregate_bcast_skip) is
+    np.average of the replicas' rows; the fused form is held bit-identical to it below."""
     import torch
-    st = engine.trainer.prepare([(0, 1, 2)], 1)
+    keep = engine.fuse_avg
+    engine.fuse_avg = False
+    try:
+        st = engine.trainer.prepare([(0, 1, 2)], 1)
+    finally:
+        engine.fuse_avg = keep
     for s in range(st.round_len):
         st.step(s)
     before = st.params.cpu().numpy().copy()
@@ -184,6 +191,47 @@ def test_fedavg_aggregation_inside_training_is_np_average(scenario, engine):
     st.step(st.round_len)  # first step of round 2: every replica sources W3 from coalition row 0
     torch.cuda.synchronize()
     assert st.ws["w3src"].cpu().tolist() == [0, 0, 0]
+
+
+def test_fused_w3_average_is_bit_identical(scenario, engine):
+    """VERDICT r5 item 8 (ABI 4): the round's last step averaging W3 in its dense pass (dense1_bwd_adam_avg_kernel,
+    then mplc_fedavg_aggregate_skip for the other layers) gives the coalition rows of the separate aggregation bit
+    for bit, round after round - also with members that finish their round's fit a step early (ragged partner
+    sizes: 8 vs 9 Keras steps) - and the same v(S), models and replica rows outside W3."""
+    import itertools
+    import torch
+    from mplc.engine import CoalitionEngine
+    sc = make_scenario(partners=5, amounts=(0.1, 0.15, 0.2, 0.25, 0.3), M=3, G=8, E=2)
+    eng = CoalitionEngine.for_scenario(sc, memory_budget_bytes=8 << 30, eval_budget_bytes=1 << 30)
+    coals = [c for k in (1, 2, 3, 5) for c in itertools.combinations(range(5), k)]
+    runs = {}
+    for fuse in (False, True):
+        eng.fuse_avg = fuse
+        st = eng.trainer.prepare(coals, 2)
+        assert (st.avg["n"] > 0) == fuse
+        globs = []
+        for s in range(st.total_steps):
+            st.step(s)
+            if st.fed_steps and s < st.fed_steps and (s + 1) % st.round_len == 0:
+                st.aggregate(epoch_end=(s + 1) % (eng.minibatch_count * st.round_len) == 0)
+                torch.cuda.synchronize()
+                globs.append(st.glob.cpu().numpy().copy())
+        torch.cuda.synchronize()
+        runs[fuse] = (globs, st.params.cpu().numpy().copy(), st.R)
+        del st
+    assert all(np.array_equal(a, b) for a, b in zip(runs[False][0], runs[True][0])), "coalition rows differ"
+    lo, hi = eng.model_impl.BCAST_SKIP
+    pa, pb = runs[False][1], runs[True][1]
+    assert np.array_equal(pa[:, :lo], pb[:, :lo]) and np.array_equal(pa[:, hi:], pb[:, hi:])
+    steps = {-(-(eng.bounds[p][m + 1] - eng.bounds[p][m]) // eng.batch_sizes[p]) for p in range(5)
+             for m in range(eng.minibatch_count)}
+    assert len(steps) > 1, steps  # ragged: some members idle at the round's last step
+    eng.fuse_avg = False
+    v0 = eng.evaluate(coals, return_details=True, return_models=True)
+    eng.fuse_avg = True
+    v1 = eng.evaluate(coals, return_details=True, return_models=True)
+    assert np.array_equal(v0["scores"], v1["scores"])
+    assert all(np.array_equal(a, b) for m0, m1 in zip(v0["models"], v1["models"]) for a, b in zip(m0, m1))
 
 
 def test_eval_loss_independent_of_models_sharing_the_evaluation(engine):

@@ -57,10 +57,14 @@ def test_argument_errors_without_gpu():
 
 def test_abi_version_bumped_with_the_cifar_layout():
     # version 2: MPLC_CIFAR_WT grew to 114688 (Winograd weights) and the layout queries were added; version 3: the
-    # pooled-gradient slots dz4 / dz2 shrank to their pooled sizes
-    assert _native.ABI_VERSION == 3
+    # pooled-gradient slots dz4 / dz2 shrank to their pooled sizes; version 4: mplc_cnn_train_t's fused W3 average
+    # (avg_*) and mplc_fedavg_aggregate_skip
+    assert _native.ABI_VERSION == 4
     text = open(os.path.join(REPO, "include", "mplc_hip.h")).read()
-    assert re.search(r"#define MPLC_ABI_VERSION 3\b", text)
+    assert re.search(r"#define MPLC_ABI_VERSION 4\b", text)
+    assert "mplc_fedavg_aggregate_skip" in text
+    cnn = open(os.path.join(REPO, "include", "mplc_hip_cnn.h")).read()
+    assert all(f in cnn for f in ("avg_first", "avg_w", "avg_scale", "avg_glob", "avg_out", "avg_rep"))
     defs = _header_defines("mplc_hip_cifar.h")
     assert (defs["MPLC_CIFAR_DZ4"], defs["MPLC_CIFAR_DZ2"]) == (6 * 6 * 64, 15 * 15 * 32)
 
