@@ -341,6 +341,95 @@ __global__ __launch_bounds__(NW * 64) void conv_kernel(const ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// conv1 forward (3 input channels, 'same', 32 output channels + ReLU; round 6): the implicit
+// GEMM of conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD> with the operands' roles swapped - the output channels
+// are the M rows of v_mfma_f32_32x32x2f32 (A = W1 transposed: lane (co, kh) holds W1[k][co], k = 2s + kh, loaded
+// once for all 14 k-steps) and the band's pixels its N columns (B = the staged image, the same LDS reads).  Every
+// output is the same fmaf chain over k = 0 .. 27 as before (a product's operands only trade places): bit-identical.
+// What changes is the epilogue: a lane's 16 accumulators are 4 runs of 4 consecutive channels of ONE pixel (C/D
+// rows 8j + 4kh .. +3), so the bias is 4 x 16-B loads per lane for the whole block, the ReLU'd activations leave as
+// 4 x 16-B stores per tile (16 x 4-B stores and per-register pixel arithmetic before), and no tile needs a bounds
+// test (4 bands x 2 x 4 tiles of 4 x 8 pixels cover the 32 x 32 output exactly).  conv1 is HBM-bound (K = 27:
+// 12.3 flop/B): the stores are what it is made of.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(const ConvArgs a) {
+  constexpr int HI = 32, WI = 32, CI = 3, CO = 32, PAD = 1, BR = 8, NW = 4, UM = 2;
+  constexpr int WO = WI, TX = WO / 8;  // 4 x 8-pixel tiles across, 2 down per band
+  constexpr int LR = BR + 2, WIP = WI + 2 * PAD, CIP = CI;
+  constexpr int ROWP = WIP * CIP + ((8 - (WIP * CIP) % 32) + 32) % 32;
+  static_assert(NW * UM == TX * (BR / 4), "the band's tiles, one per (wave, u)");
+  __shared__ float in_s[LR * ROWP];
+  const int band = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+  const int count = a.cnt ? a.cnt[r] : a.cnt_all;
+  if (j >= count) return;
+  const int tid = threadIdx.x;
+  const int64_t slot = (int64_t)r * a.bmax + j;
+  constexpr int IN_SZ = HI * WI * CI;
+  const float* src = a.in_mode == 1 ? a.in + (int64_t)a.idx[slot] * IN_SZ
+                     : a.in_mode == 2 ? a.in + (int64_t)(a.row_base + j) * IN_SZ
+                                      : a.in + slot * IN_SZ;
+  const int y0 = band * BR;
+  {  // the band's 10 input rows (zero padded), as conv_kernel stages them
+    constexpr int TOT = LR * WIP * CI;
+    constexpr int NIT = (TOT + 255) / 256;
+    float v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + k * 256;
+      const int c = e % CI, pix = e / CI;
+      const int iy = y0 - PAD + pix / WIP, ix = pix % WIP - PAD;
+      const bool ok = e < TOT && iy >= 0 && iy < HI && ix >= 0 && ix < WI;
+      const float t = *(ok ? src + (iy * WI + ix) * CI + c : src);
+      v[k] = ok ? t : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int e = tid + k * 256;
+      if (e < TOT) {
+        const int c = e % CI, pix = e / CI;
+        in_s[(pix / WIP) * ROWP + (pix % WIP) * CIP + c] = v[k];
+      }
+    }
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31, kh = lane >> 5;
+  // A operand: W1[k][co = n] for k = 2s + kh (0 past k = 26), the same for both tiles
+  const float* W = a.w + (int64_t)r * a.w_rstride;
+  float wa[14];
+#pragma unroll
+  for (int s = 0; s < 14; ++s) wa[s] = (2 * s + kh) < 27 ? W[(2 * s + kh) * CO + n] : 0.0f;
+  const float* bias = a.bias + (int64_t)r * a.b_rstride;
+  fvec4 bv[4];  // channels 8 jj + 4 kh .. + 3
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) bv[jj] = *reinterpret_cast<const fvec4*>(bias + 8 * jj + 4 * kh);
+  __syncthreads();
+  float* o = a.out + slot * (WO * WO * CO);
+#pragma unroll
+  for (int u = 0; u < UM; ++u) {
+    const int t = wave + NW * u;
+    const int ty = t / TX, tx = t % TX;
+    const int yl = ty * 4 + n / 8, x = tx * 8 + n % 8;  // this lane's pixel (column n of the tile)
+    const int ab = yl * ROWP + x * CIP;
+    floatx16 acc = zero16();
+#pragma unroll
+    for (int s = 0; s < 14; ++s) {
+      const int k = 2 * s + kh;
+      const int off = kh ? (2 * s + 1 < 27 ? ci3_off(2 * s + 1, ROWP) : 0) : ci3_off(2 * s, ROWP);
+      const float bx = k < 27 ? in_s[ab + off] : 0.0f;
+      acc = mfma32(wa[s], bx, acc);
+    }
+    fvec4* op = reinterpret_cast<fvec4*>(o + ((y0 + yl) * WO + x) * CO + 4 * kh);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      fvec4 z;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z[i] = fmaxf(acc[4 * jj + i] + bv[jj][i], 0.0f);
+      op[2 * jj] = z;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // 3x3 stride-1 convolution in Winograd form F(2x2, 3x3) (Lavin & Gray) on v_mfma_f32_16x16x4_f32, for the
 // layers with CI >= 32 (conv2..conv4 forward, and their data gradients = forward convolutions of dZ with the
 // rotated, channel-swapped kernel, padding 2 - PAD):
@@ -2115,7 +2204,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // layer instantiations: <HI, WI, CI, CO, PAD, BR, NW, UM, EPI> (conv) and <HI, WI, CI, CO, PAD, HOV, WOV,
 // BR, NW> (wgrad); geometry checked by static_asserts, LDS per block in the comment
 // ------------------------------------------------------------------------------------------------
-#define CONV1_FWD conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD>          /* 4 bands,  4.1 KB */
+#define CONV1_FWD conv1_fwd_kernel  /* 4 bands, 4.1 KB; conv_kernel<32, 32, 3, 32, 1, 8, 4, 2, EPI_FWD> with the channels as M rows */
 // Winograd F(2x2,3x3): <HI, WI, CI, CO, PAD, tile rows per band, EPI>; bands = ceil(tile rows / BTY)
 // wave-local form: <HI, WI, CI, CO, PAD, BTY, waves, EPI>; reads conv2's Winograd weights in the xi-last layout
 #define CONV2_FWD wino_wl_kernel<32, 32, 32, 32, 0, 4, 4, EPI_FWD_POOL>      /* 60 tiles, 4 bands, 42 KB */

@@ -78,7 +78,8 @@ EVAL_SAMPLE_IO = {"conv1_fwd": _F * (IMG_FLOATS + A1), "conv2_fwd": _F * (A1 + D
                   "conv4_fwd": _F * (A3 + D4), "dense5_fwd": _F * (D4 + H5)}
 EVAL_CHUNK_IO = {"conv2_fwd": _F * _U2, "conv3_fwd": _F * _U3, "conv4_fwd": _F * _U4, "dense5_fwd": _F * (D4 * H5 + H5)}
 # rocprofv3 kernel names (template instances, csrc/cifar_cnn.hip CONV* macros) -> the step's launch names
-KERNEL_NAME_PREFIX = (("conv_kernel<32, 32, 3, 32", "conv1_fwd"), ("wino_wl_kernel<32, 32, 32, 32", "conv2_fwd"),
+KERNEL_NAME_PREFIX = (("conv1_fwd_kernel", "conv1_fwd"), ("conv_kernel<32, 32, 3, 32", "conv1_fwd"),
+                      ("wino_wl_kernel<32, 32, 32, 32", "conv2_fwd"),
                       ("wino_kernel<15, 15, 32, 64", "conv3_fwd"), ("wino_kernel<15, 15, 64, 64", "conv4_fwd"),
                       ("dense5_fwd16_kernel", "dense5_fwd"), ("dense5_fwd_kernel", "dense5_fwd"),
                       ("head_kernel", "head"), ("dense5_bwd_kernel", "dense5_bwd"),

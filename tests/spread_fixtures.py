@@ -59,6 +59,28 @@ def config4_scenario(epochs=1):
                     gradient_updates_per_pass_count=8, epoch_count=epochs, is_early_stopping=False).provision()
 
 
+# tests/test_ranking_gpu.py: the 10-partner exact-Shapley ranking scenario, chosen with scripts/probe_ranking.py
+# (profiles/r06_probe_ranking_grid4.log: the ranking unchanged under five ~1-ulp perturbations of the training data,
+# every adjacent Shapley gap >= 2.25x the spread of the difference): MNIST-shaped synthetic data (class templates,
+# signal 0.25, 1000 test images), dataset_proportion 0.1, random split over unequal amounts (np.sum == 1.0 exactly,
+# the reference's assert mplc/scenario.py:587-590), FedAvg E=4, M=1, G=32 (one round per epoch: the sequential CPU
+# oracle's sweep of all 1023 coalitions is ~0.7 M optimizer steps)
+RANKING = {"amounts": [0.02, 0.03, 0.04, 0.06, 0.08, 0.10, 0.12, 0.15, 0.18, 0.22], "signal": 0.25,
+           "dataset_proportion": 0.1, "n_test": 1000, "epoch_count": 4, "minibatch_count": 1,
+           "gradient_updates_per_pass_count": 32, "split": "random"}
+
+
+def ranking_scenario():
+    from mplc.dataset import Mnist
+    from mplc.scenario import Scenario
+    p = RANKING
+    return Scenario(10, list(p["amounts"]), dataset=Mnist(synthetic=True, signal=p["signal"], n_test=p["n_test"]),
+                    dataset_proportion=p["dataset_proportion"], samples_split_option=["basic", p["split"]],
+                    minibatch_count=p["minibatch_count"],
+                    gradient_updates_per_pass_count=p["gradient_updates_per_pass_count"],
+                    epoch_count=p["epoch_count"], is_early_stopping=False).provision()
+
+
 def scenario(name):
     if name == "config1_3p":
         sc = config1_scenario([0.2, 0.5, 0.3])

@@ -1,0 +1,51 @@
+"""GPU: partner ranking at the 10-partner exact-Shapley scale (north_star: "Partner ranking: must
+be identical"; the reference's exact path mplc/contributivity.py:140-171, 1210-1253, and its only ranking
+assertion tests/end_to_end_tests.py:66-73, ported at 2 partners in tests/test_cnn_gpu.py / test_config1_gpu.py).
+
+The fixture tests/golden/ranking_10p.json (scripts/ranking_fixture.py, build container) holds the CNN oracle's v(S)
+for all 1023 coalitions of tests/spread_fixtures.py ranking_scenario - each trained the reference's way, one after
+the other (oracle/cnn.py) - and the Shapley values of the reference's shapley_value restated in its fp64 order.
+Here the product computes the same thing: Contributivity.compute_contributivity("Shapley values") on the HIP engine
+(all 1023 coalitions in one lockstep batch, the bitmask Shapley kernel).  Gates:
+  - argsort of the device's Shapley values == argsort of the oracle's (the ranking identical);
+  - every |SV_device - SV_oracle| <= SV_BOUND (declared below), and Sum SV = v(N) to 1e-12 (efficiency);
+  - v(S) itself: the mean signed difference over the 1023 coalitions within 1 pt (no bias).
+The scenario was chosen on the GPU (scripts/probe_ranking.py) for a ranking that survives ~1-ulp perturbations of
+the training data with every adjacent Shapley gap several times their spread: the device differs from the oracle
+by fp32 summation order, a perturbation of that size."""
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SV_BOUND = 0.015  # per partner, |SV_device - SV_oracle| (the perturbation spread of the probe, x 2.5)
+
+
+def test_ten_partner_exact_shapley_ranking_identical_to_oracle():
+    from spread_fixtures import GOLDEN, data_crc, ranking_scenario
+    from mplc.contributivity import Contributivity
+    with open(os.path.join(GOLDEN, "ranking_10p.json")) as f:
+        rec = json.load(f)
+    sc = ranking_scenario()
+    assert rec["data_crc32"] == data_crc(sc), "ranking_10p.json was made for other data"
+    assert [len(p.train_idx) for p in sc.partners_list] == rec["partner_rows"]
+    c = Contributivity(scenario=sc)
+    c.compute_contributivity("Shapley values")
+    assert c.first_charac_fct_calls_count == 1023
+    sv_dev = np.asarray(c.contributivity_scores, dtype=np.float64)
+    sv_ref = np.asarray(rec["shapley"], dtype=np.float64)
+    n = len(sv_ref)
+    coals = [k for r in range(1, n + 1) for k in itertools.combinations(range(n), r)]
+    v_dev = np.array([c.charac_fct_values[k] for k in coals])
+    v_ref = np.array([rec["values_bitmask"][sum(1 << p for p in k)] for k in coals])
+    v_all = c.charac_fct_values[tuple(range(n))]
+    print("device SV", np.round(sv_dev, 4).tolist(), "oracle SV", np.round(sv_ref, 4).tolist())
+    print("v(S) mean signed diff %.4f, max |diff| %.4f" % (np.mean(v_dev - v_ref), np.max(np.abs(v_dev - v_ref))))
+    assert abs(np.sum(sv_dev) - v_all) <= 1e-12 * max(1.0, abs(v_all))
+    assert np.argsort(sv_dev).tolist() == rec["argsort"], (np.argsort(sv_dev).tolist(), rec["argsort"])
+    assert np.max(np.abs(sv_dev - sv_ref)) <= SV_BOUND, (sv_dev - sv_ref)
+    assert abs(np.mean(v_dev - v_ref)) <= 0.01
