@@ -843,7 +843,10 @@ def bench_cifar(args, rank, world, sub=False):
         "kernel_timer": {"batches_timed": sampled["timed"], "batches": sampled["batches"],
                          "replica_steps_timed": sampled["timed_replica_steps"],
                          "replica_steps": sampled["replica_steps"],
-                         "note": f"in-stream HIP events around every launch of one lockstep batch in {CIFAR_TIMER_EVERY}; "
+                         "streams": eng.concurrent_batches,
+                         "note": f"in-stream HIP events around every launch of one lockstep batch in {CIFAR_TIMER_EVERY}, "
+                                 "which runs as ONE batch on one stream (the others in two halves on two HIP streams, "
+                                 "the CIFAR10 default: CnnBatchTrainer.run_concurrent); "
                                  "value covers the whole run, timed and untimed batches"},
     }
     # the roofline on the step's dominant kernel (largest share of the kernel time), as the config #3 line
