@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/profile_$1
 R=/tmp/profile_$1
 [ "$2" = pmc ] || rm -rf $O $R; mkdir -p $O $R
-K='conv_bwd_data_kernel|conv_fwd_kernel|conv_wgrad_kernel|dense1_bwd_adam_kernel|dense_fwd_kernel|shapley_block_kernel'
+K='conv_bwd_data_kernel|conv_fwd_kernel|conv_wgrad_kernel|dense1_bwd_adam_kernel|dense1_bwd_adam_avg_kernel|dense_fwd_kernel|shapley_block_kernel'
 CMD="python bench.py --steps 1 --warmup 1 --no-cpu-baseline"
 # the counter passes run without the bench's in-stream HIP events (a --pmc pass with an event record around
 # every launch crashed rocprofv3's counter thread: SIGSEGV, gpurun_out/profile_r02v6/fetch.err) and without
