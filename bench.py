@@ -137,6 +137,20 @@ def pmc_entry(kernel, workload):
     return None
 
 
+def pmc_by_launch(name, workload):
+    """config #4: the counters' bytes of launch `name` (mplc.cifar.launch_name: conv2_fwd, dense5_bwd, ...) over
+    every launch of the profiled run beside its compulsory bytes (profiles/pmc_traffic_config4.json by_launch)."""
+    for fname in PMC_FILES:
+        try:
+            with open(os.path.join(REPO, "profiles", fname)) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("workload") == workload and name in doc.get("by_launch", {}):
+            return doc["by_launch"][name]
+    return None
+
+
 # launches timed as one entry of the kernel table: a round's last MNIST step runs dense1_bwd_adam_kernel for the
 # unfused replicas and dense1_bwd_adam_avg_kernel for the fused coalitions between the same two events (ABI 4)
 PMC_FOLD = {"dense1_bwd_adam_kernel": ("dense1_bwd_adam_avg_kernel",)}
@@ -872,6 +886,9 @@ def bench_cifar(args, rank, world, sub=False):
                 e["traffic_pmc"] = int(pe["traffic_bytes_per_launch"])
                 if pe.get("algorithmic_bytes_per_launch"):
                     e["traffic_over_algorithmic"] = round(pe["traffic_bytes_per_launch"] / pe["algorithmic_bytes_per_launch"], 4)
+            pb = pmc_by_launch(k, wl)  # every kernel, either bound: counter bytes / compulsory bytes, all launches
+            if pb is not None and pb.get("traffic_over_compulsory"):
+                e["pmc_traffic_over_compulsory"] = round(pb["traffic_over_compulsory"], 4)
         out["roofline_conv2_fwd"] = out["roofline"]
         out["roofline"] = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
                            "frac": kd["frac"], "traffic": kd.get("traffic_pmc"),

@@ -485,7 +485,7 @@ __device__ __forceinline__ void unpool_load(const float* __restrict__ pooled, co
     cw[k] = c;
   }
 }
-template <int C, int NR, int NC, int CP, int NTHR>
+template <int C, int NR, int NC, int CP, int NTHR, int RS = NC * CP>  // RS: the image's row stride (floats)
 __device__ __forceinline__ void unpool_store(float* __restrict__ dst, int tid,
                                              const fvec4 (&val)[UnpoolShape<C, NR, NC, NTHR>::NIT],
                                              const uint32_t (&cw)[UnpoolShape<C, NR, NC, NTHR>::NIT]) {
@@ -495,10 +495,10 @@ __device__ __forceinline__ void unpool_store(float* __restrict__ dst, int tid,
     const int e = tid + k * NTHR;
     if (e < S::TOT) {
       const int win = e / S::C4, c4 = e % S::C4;
-      float* d0 = dst + ((2 * (win / (NC / 2))) * NC + 2 * (win % (NC / 2))) * CP + 4 * c4;
+      float* d0 = dst + (2 * (win / (NC / 2))) * RS + (2 * (win % (NC / 2))) * CP + 4 * c4;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        float* d = d0 + ((p >> 1) * NC + (p & 1)) * CP;
+        float* d = d0 + (p >> 1) * RS + (p & 1) * CP;
         d[0] = (cw[k] & 3) == (uint32_t)p ? val[k].x : 0.0f;
         d[1] = ((cw[k] >> 8) & 3) == (uint32_t)p ? val[k].y : 0.0f;
         d[2] = ((cw[k] >> 16) & 3) == (uint32_t)p ? val[k].z : 0.0f;
@@ -507,14 +507,14 @@ __device__ __forceinline__ void unpool_store(float* __restrict__ dst, int tid,
     }
   }
 }
-template <int HP, int WP, int C, int NR, int NC, int CP, int NTHR>
+template <int HP, int WP, int C, int NR, int NC, int CP, int NTHR, int RS = NC * CP>
 __device__ __forceinline__ void stage_unpool(const float* __restrict__ pooled, const uint8_t* __restrict__ codes,
                                              int iy0, int ix0, float* __restrict__ dst, int tid) {
   using S = UnpoolShape<C, NR, NC, NTHR>;
   fvec4 val[S::NIT];
   uint32_t cw[S::NIT];
   unpool_load<HP, WP, C, NR, NC, NTHR>(pooled, codes, iy0, ix0, tid, val, cw);
-  unpool_store<C, NR, NC, CP, NTHR>(dst, tid, val, cw);
+  unpool_store<C, NR, NC, CP, NTHR, RS>(dst, tid, val, cw);
 }
 
 __device__ __forceinline__ void wino_g_rows(const float (&g)[3], float (&o)[4]) {  // o = G g (one column)
@@ -659,7 +659,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int NG = (BTY * TXT + 15) / 16;      // 16-tile groups per band
   constexpr int LR = 2 * BTY + 2, LC = 2 * TXT + 2;
   constexpr int CIP = CI + 1;                    // odd channel stride
-  constexpr int ROWP = LC * CIP;
+  // Row stride padded to ROWP = TXT (mod 16): with CIP = 1 (mod 16) tile (tyl, tx) then starts on bank
+  // 2 (TXT tyl + tx) = 2 tile (mod 32), so a half-wave's 16 tiles x 2 channels (kq) fill the 32 banks once (the
+  // unpadded LC CIP put a group's second tile row on its first row's banks: 2-way conflicts on every V read)
+  constexpr int ROWP = LC * CIP + ((TXT - LC * CIP) % 16 + 16) % 16;
+  static_assert(CIP % 16 == 1 && ROWP % 16 == TXT % 16, "conflict-free V reads");
   constexpr int NCG = CO / 16;
   constexpr int CH = CO > 32 ? 32 : CO;          // output channels per output-transform pass
   constexpr int NPASS = CO / CH;
@@ -693,8 +697,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int ntile = bty * TXT;
   if constexpr (UPI) {  // the input is a POOLED gradient [HI/2][WI/2][CI] with its pool codes: un-pooled here
     static_assert(PAD % 2 == 0 && LR % 2 == 0 && LC % 2 == 0, "the staged region must be whole pooling windows");
-    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, 256>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
-                                                       2 * ty0 - PAD, -PAD, in_s, tid);
+    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, 256, ROWP>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
+                                                             2 * ty0 - PAD, -PAD, in_s, tid);
   } else {  // stage input rows 2 ty0 - PAD .. + LR, columns -PAD .. + LC (zero outside the input)
     constexpr int C4 = CI / 4;
     constexpr int TOT = LR * LC * C4;
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int e4 = tid + k * 256;
       if (e4 < TOT) {
         const int pix = e4 / C4, c4 = e4 % C4;
-        float* d = in_s + pix * CIP + 4 * c4;
+        float* d = in_s + (pix / LC) * ROWP + (pix % LC) * CIP + 4 * c4;
         d[0] = v[k].x;
         d[1] = v[k].y;
         d[2] = v[k].z;
@@ -803,7 +807,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto quad_group = [&](int t0, fvec4 (&q)[4]) __attribute__((always_inline)) {
     const int tile = t0 + (lane & 3);
     const int tyl = tile / TXT, tx = tile % TXT;
-    const float* dpa = in_s + ((2 * tyl + ry) * LC + 2 * tx) * CIP;
+    const float* dpa = in_s + (2 * tyl + ry) * ROWP + 2 * tx * CIP;
     const float* Uq = a.w + (int64_t)r * a.w_rstride + (int64_t)(4 * wi) * CI * CO + (lane & (CO - 1));
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) q[jj] = fvec4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     } else {
     const int tile = min(16 * g + tl, ntile - 1);
     const int tyl = tile / TXT, tx = tile % TXT;
-    const float* dpa = in_s + ((2 * tyl + ry) * LC + 2 * tx) * CIP + kq;
+    const float* dpa = in_s + (2 * tyl + ry) * ROWP + 2 * tx * CIP + kq;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
@@ -1215,7 +1219,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   constexpr int TXT = POOL ? PW : (WO + 1) / 2;
   constexpr int LR = 2 * BTY + 2, LC = 2 * TXT + 2;
   constexpr int CIP = CI + 1;
-  constexpr int ROWP = LC * CIP;
+  constexpr int ROWP = LC * CIP + ((TXT - LC * CIP) % 16 + 16) % 16;  // conflict-free V reads, as wino_kernel's
+  static_assert(CIP % 16 == 1 && ROWP % 16 == TXT % 16, "conflict-free V reads");
   constexpr int NK = CI / 4;
   constexpr int NTHR = NW * 64;
   static_assert(CO == 32 && CI % 8 == 0, "wave-local form: 32 output channels");
@@ -1234,8 +1239,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int ntile = bty * TXT;
   if constexpr (UPI) {  // the input is a POOLED gradient [HI/2][WI/2][CI] with its pool codes: un-pooled here
     static_assert(PAD % 2 == 0 && LR % 2 == 0 && LC % 2 == 0, "the staged region must be whole pooling windows");
-    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, NTHR>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
-                                                        2 * ty0 - PAD, -PAD, in_s, tid);
+    stage_unpool<HI / 2, WI / 2, CI, LR, LC, CIP, NTHR, ROWP>(src, a.code_in + slot * ((HI / 2) * (WI / 2) * CI),
+                                                              2 * ty0 - PAD, -PAD, in_s, tid);
   } else {
     constexpr int C4 = CI / 4;
     constexpr int TOT = LR * LC * C4;
@@ -1254,7 +1259,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     for (int k = 0; k < NIT; ++k) {
       const int e4 = tid + k * NTHR;
       if (e4 < TOT) {
-        float* d = in_s + e4 / C4 * CIP + 4 * (e4 % C4);
+        const int pix = e4 / C4;
+        float* d = in_s + (pix / LC) * ROWP + (pix % LC) * CIP + 4 * (e4 % C4);
         d[0] = v[k].x;
         d[1] = v[k].y;
         d[2] = v[k].z;
@@ -1267,7 +1273,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (16 * wave >= ntile) return;  // wave-uniform; no barrier follows
   const int tl = lane & 15, kq = lane >> 4;
   const int tile = min(16 * wave + tl, ntile - 1);
-  const float* dpa = in_s + ((2 * (tile / TXT)) * LC + 2 * (tile % TXT)) * CIP + kq;
+  const float* dpa = in_s + (2 * (tile / TXT)) * ROWP + 2 * (tile % TXT) * CIP + kq;
   // B operands of k-step st: U[4 st + kq][16 cg + tl][xi] (the xi-last layout of wino_u_kernel's conv2 section):
   // a lane's 16 transform points of one channel pair are 64 contiguous bytes, 4 x 16-B loads per cg
   const fvec4* Ub = reinterpret_cast<const fvec4*>(a.w + (int64_t)r * a.w_rstride) + (kq * CO + tl) * 4;
@@ -1805,7 +1811,11 @@ __global__ __launch_bounds__(256) void dense5_fwd16_kernel(const float* __restri
                                                            const int32_t* __restrict__ w5src,
                                                            const uint64_t* __restrict__ drop_key,
                                                            float* __restrict__ H, uint8_t* __restrict__ code) {
-  __shared__ float a_s[16 * (DF_K + 1)];
+  // A rows at a stride of DF_K + 2 (round 6): a half-wave's ds_read_b32 takes rows tl = 0..15 at
+  // k-offsets kq and kq + 1, banks 2 tl + kq: 32 distinct (DF_K + 1 put row tl + 1's kq on row tl's kq + 1: 2-way,
+  // PMC conflict ratio 0.44).  Layout only: bit-identical.
+  constexpr int AS = DF_K + 2;
+  __shared__ float a_s[16 * AS];
   const LogicalBlock lbk = xcd_block3();  // (sample tile, column slice, replica): a replica's W5 in one XCD's L2
   const int r = lbk.z;
   const int m0 = lbk.x * 16;
@@ -1840,7 +1850,7 @@ __global__ __launch_bounds__(256) void dense5_fwd16_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < AIT; ++i) {
       const int e = tid + 256 * i;
-      a_s[(e / DF_K) * (DF_K + 1) + e % DF_K] = av[i];
+      a_s[(e / DF_K) * AS + e % DF_K] = av[i];
     }
     float bc[DF_K / 4];
 #pragma unroll
@@ -1848,7 +1858,7 @@ __global__ __launch_bounds__(256) void dense5_fwd16_kernel(const float* __restri
     load(min(k0 + DF_K, FEAT - DF_K));  // the last chunk re-loads itself (uniform, branch-free)
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < DF_K / 4; ++s) acc = mfma16(a_s[tl * (DF_K + 1) + 4 * s + kq], bc[s], acc);
+    for (int s = 0; s < DF_K / 4; ++s) acc = mfma16(a_s[tl * AS + 4 * s + kq], bc[s], acc);
   }
   const int col = n0 + tl;
   const float bias = params[(int64_t)r * stride + OFF_B5 + col];

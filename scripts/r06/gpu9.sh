@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+bash scripts/r06/gpu_copylog.sh > gpurun_out/r06_copylog.txt 2>&1 && \
+bash scripts/r06/gpu_pmc_cifar.sh > gpurun_out/r06_pmc4.txt 2>&1
