@@ -382,6 +382,7 @@ class Contributivity:
                 rows[t - 1][perm[j]] = chars[j + 1] - chars[j]
             v_max = np.max(np.var(rows[:t], axis=0))
         contributions = rows[:t]
+        self.mc_walks = t  # permutations the estimator consumed (the waves may have drawn more)
         return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1)
 
     def truncated_MC(self, sv_accuracy=0.01, alpha=0.9, truncation=0.05):
@@ -456,6 +457,7 @@ class Contributivity:
                 rows[t - 1][k] = increment * renorms[k] / np.abs(approx_for(tuple(int(i) for i in S), k))
             v_max = np.max(np.var(rows[:t], axis=0))
         contributions = rows[:t]
+        self.mc_walks = t  # permutations the estimator consumed (the waves may have drawn more)
         return np.mean(contributions, axis=0), np.std(contributions, axis=0) / np.sqrt(t - 1)
 
     @staticmethod

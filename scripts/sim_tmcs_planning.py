@@ -44,8 +44,9 @@ def load_table(path, n):
     return value, len(vals)
 
 
-def run(n, value, method, target, wave_scale=1, adaptive=True, margin=0.5):
+def run(n, value, method, target, wave_scale=1, adaptive=True, margin=0.5, world=1):
     batches = []
+    Contributivity._world_size = lambda self: world  # the planner's per-rank targets and wave scale at N ranks
 
     class Approach:
         device_planning = False
@@ -74,23 +75,27 @@ def main():
     ap.add_argument("--targets", default="0,256,512,1024,2048,4096")
     ap.add_argument("--margins", default="16", help="mc_plan_overhead values")
     ap.add_argument("--cost", default="0.09,0.0033", help="A,B of the per-batch time model (s, s per replica)")
+    ap.add_argument("--world", type=int, default=1, help="ranks: a batch costs A + B * replicas / world")
+    ap.add_argument("--scales", default="0", help="mc_wave_scale values (0: the world size)")
     args = ap.parse_args()
     A, B = (float(x) for x in args.cost.split(","))
     value, held = load_table(args.values, args.n)
     ref = None
-    for target, adaptive, margin in [(int(t), a, float(m)) for a in (False, True) for t in args.targets.split(",")
-                                     for m in args.margins.split(",")]:
-        c, batches, trained = run(args.n, value, args.method, target, adaptive=adaptive, margin=margin)
+    for target, adaptive, margin, scale in [(int(t), a, float(m), int(w)) for a in (False, True)
+                                            for t in args.targets.split(",") for m in args.margins.split(",")
+                                            for w in args.scales.split(",")]:
+        c, batches, trained = run(args.n, value, args.method, target, adaptive=adaptive, margin=margin,
+                                  world=args.world, wave_scale=scale)
         if ref is None:
             ref = c.contributivity_scores
         assert np.array_equal(ref, c.contributivity_scores)  # speculation never changes the result
         reps = np.array(batches)
-        est = len(reps) * A + reps.sum() * B
-        print(f"{'adaptive' if adaptive else 'fixed   '} target {target:5d} overhead {margin}: batches {len(reps):4d}  replicas/batch {reps.mean():7.1f} (median "
+        est = len(reps) * A + np.ceil(reps / args.world).sum() * B
+        print(f"{'adaptive' if adaptive else 'fixed   '} scale {scale} target {target:5d} overhead {margin}: batches {len(reps):4d}  replicas/batch {reps.mean():7.1f} (median "
               f"{np.median(reps):6.0f})  counted {c.first_charac_fct_calls_count}  trained {trained}  "
               f"(+{100 * (trained / c.first_charac_fct_calls_count - 1):.1f} %)  replicas {reps.sum()}  "
               f"est {est:6.1f} s -> {c.first_charac_fct_calls_count / est:6.1f} evals/s  "
-              f"plan {getattr(c, 'plan_stats', {})}", flush=True)
+              f"walks {getattr(c, 'mc_walks', None)} plan {getattr(c, 'plan_stats', {})}", flush=True)
 
 
 if __name__ == "__main__":
