@@ -438,7 +438,15 @@ __device__ __forceinline__ void adam_first_moments(float g, const AdamCfg& c, fl
   v1 = __fmul_rn(1.0f - c.b2, __fmul_rn(g, g));
 }
 
+// Every operation rounded on its own, in Keras' order (keras/optimizers.py Adam.get_updates; oracle/cnn.py
+// KerasAdam): m_t = (b1 m) + ((1 - b1) g), v_t = (b2 v) + ((1 - b2) g^2), p - (lr_t m_t) / (sqrt(v_t) + eps).  Under
+// hipcc's default fp-contract=fast, `b1 * m + (1 - b1) * g` may become fma(b1, m, (1 - b1) g) OR fma(1 - b1, g, b1 m)
+// - two roundings of the same sum, and which one the backend picks depended on the code around the inlined call: a
+// refactor of dense1_bwd_adam_kernel that left its FP instruction multiset unchanged moved the MNIST models in their
+// last bits (profiles/r06_adam_contraction.txt).  Contraction off here (as rms_apply, cifar_common.h; the __*_rn
+// intrinsics do not stop the backend fusing) pins one rounding per operation.
 __device__ __forceinline__ void adam_apply(float& p, float& m, float& v, float g, const AdamCfg& c) {
+#pragma clang fp contract(off)
   float mt, vt;
   if (c.reset) {
     adam_first_moments(g, c, mt, vt);
