@@ -21,8 +21,12 @@ LIB_DIR = os.path.join(PKG_ROOT, "mplc", "lib")
 LIB = os.path.join(LIB_DIR, "libmplc_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# -ffp-contract=on: multiply-adds fuse only within one source expression, as the source writes them (hipcc's default
+# also lets the backend fuse across statements, and which product it picks can move with unrelated code: a refactor of
+# dense1_bwd_adam_kernel flipped Adam's fusion, profiles/r06_adam_contraction.txt); `#pragma clang fp contract(off)`
+# still marks the code whose every operation rounds on its own (Adam, RMSprop, FedAvg)
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
-          "-Wno-unused-result", "-munsafe-fp-atomics"]
+          "-Wno-unused-result", "-munsafe-fp-atomics", "-ffp-contract=on"]
 
 
 def _deps(src):

@@ -41,6 +41,17 @@ import pytest
 
 from spread_fixtures import golden_split, load_spread, oracle_values
 
+
+def _dump_rounds(tag, errs):
+    """Per-round (device, fp32-oracle) errors of a round-trajectory test, to $MPLC_TRAJ_DUMP/<tag>.json when set."""
+    import json
+    import os
+    d = os.environ.get("MPLC_TRAJ_DUMP")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{tag}.json"), "w") as f:
+            json.dump(errs, f)
+
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -172,10 +183,13 @@ def test_config1_three_partner_round_trajectories_vs_fp64(run_3p):
     The errors are bimodal (profiles/r05_diag_config1.json, all four FedAvg coalitions, 40 rounds): ~1e-6 in a
     round without a near-tie - device and fp32 oracle alike - and 1e-4 .. 1e-2 in a round where a max-pool window or
     a ReLU input near 0 breaks the other way; such rounds hit the device and the oracle at different rounds.  So the
-    gate is per coalition and tensor on the MEDIAN round: median device error <= 4x the median fp32-oracle error
-    (measured: at most 2.2x), and at most 4 of the 10 rounds with any tensor outside 4x (measured 1, 1 and 0 for
-    these coalitions; 3 for (1, 2)).  A defect of the ragged path (a short batch averaged over bs instead of its
-    count, a dropped remainder) would put every round at ~1e-1."""
+    gate is per coalition and tensor on the LOWER QUARTILE round (the clean-mode floor, the kernels' own rounding):
+    device error <= 4x the fp32 oracle's, and at most 4 of the 10 rounds with any tensor outside 4x (measured 1, 1
+    and 0 for these coalitions; 3 for (1, 2)).  A defect of the ragged path (a short batch averaged over bs instead
+    of its count, a dropped remainder) would put every round at ~1e-1.  (Through round 6 the gate sat on the median
+    round, which lies on the boundary of the two modes when about half the rounds meet a tie - config #3's (2, 9)
+    test showed a 10x swing of the median from one tie round; tests/test_workload_gpu.py.  Quartile ratios with the
+    round's final numerics 0.1 .. 1.3, profiles/r06_traj_rounds.json.)"""
     import torch
     from oracle import cnn as ocnn
     from mplc.engine import CoalitionEngine
@@ -217,11 +231,12 @@ def test_config1_three_partner_round_trajectories_vs_fp64(run_3p):
             errs.append(row)
         del st
         outliers = sum(any(r[k][0] > 4 * r[k][1] for k in r) for r in errs)
+        _dump_rounds(f"config1_{'_'.join(map(str, coal))}", errs)
         for name in ocnn.OFF:
-            med_dev = float(np.median([r[name][0] for r in errs]))
-            med_cpu = float(np.median([r[name][1] for r in errs]))
-            report.append((coal, name, med_dev, med_cpu))
-            if not med_dev <= 4 * med_cpu:
+            q_dev = float(np.percentile([r[name][0] for r in errs], 25))
+            q_cpu = float(np.percentile([r[name][1] for r in errs], 25))
+            report.append((coal, name, q_dev, q_cpu))
+            if not q_dev <= 4 * q_cpu:
                 bad.append(report[-1])
         report.append((coal, "outlier rounds", outliers))
         if outliers > 4:
