@@ -589,12 +589,15 @@ constexpr int D1_SCHUNK = 32;  // samples staged in LDS at a time
 
 // One replica's pass over one 32-row slice of W3 (the body of dense1_bwd_adam_kernel, shared with the fused
 // averaging kernel below): dp rows written, W3's moments read / written by the optimizer step, b3 updated by the
-// slice-0 block; the updated slice is returned in w (lane's fvec4 chunks c8 + 8 i) - the caller stores it.
+// slice-0 block; the updated slice is returned in w (lane's fvec4 chunks c8 + 8 i) and, when Wout is given, stored
+// there as each chunk is updated (the standalone kernel: its stores interleaved with the moments' stores, as before
+// the slice was shared - storing after the b3 update instead cost the kernel 6 %, scripts/r06/gpu22.sh).
 __device__ __forceinline__ void dense1_replica_slice(
     int r, int k0, int count, const float* __restrict__ Pool, const float* __restrict__ dH,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
-    float* __restrict__ dPool, float lr, float b1, float b2, float eps, fvec4* dh_s, float* p_s, fvec4 (&w)[4]) {
+    float* __restrict__ dPool, float lr, float b1, float b2, float eps, fvec4* dh_s, float* p_s, fvec4 (&w)[4],
+    fvec4* Wout) {
   const int tid = threadIdx.x;
   const int rowl = tid >> 3;
   // the 8 threads of a row own interleaved fvec4 chunks q = c8 + 8*i (columns 4q..4q+3): each global
@@ -690,6 +693,7 @@ __device__ __forceinline__ void dense1_replica_slice(
       vv[i][q] = v1;
     }
     w[i] = pw;
+    if (Wout) Wout[8 * i] = pw;
     if (!cfg.last) {
       if (fresh) {
         __builtin_nontemporal_store(g[i], Mr + 8 * i);
@@ -722,12 +726,10 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
   if (count == 0) return;
   if (avg_rep && avg_rep[r]) return;  // this step's pass of r belongs to dense1_bwd_adam_avg_kernel
   fvec4 w[4];
-  dense1_replica_slice(r, k0, count, Pool, dH, adam_t, bmax, params, adam_m, adam_v, stride, glob, w3src, dPool, lr,
-                       b1, b2, eps, dh_s, p_s, w);
   fvec4* W = reinterpret_cast<fvec4*>(params + (int64_t)r * stride + OFF_W3 + (int64_t)(k0 + (threadIdx.x >> 3)) * HID) +
              (threadIdx.x & 7);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) W[8 * i] = w[i];
+  dense1_replica_slice(r, k0, count, Pool, dH, adam_t, bmax, params, adam_m, adam_v, stride, glob, w3src, dPool, lr,
+                       b1, b2, eps, dh_s, p_s, w, W);
 }
 
 // The last step of a FedAvg round with the coalition's W3 average fused in.
@@ -765,7 +767,7 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_avg_kernel(
       for (int i = 0; i < 4; ++i) w[i] = W[8 * i];
     } else {
       dense1_replica_slice(r, k0, count, Pool, dH, adam_t, bmax, params, adam_m, adam_v, stride, glob, w3src, dPool,
-                           lr, b1, b2, eps, dh_s, p_s, w);
+                           lr, b1, b2, eps, dh_s, p_s, w, nullptr);
     }
     const double wr = avg_w[r];
 #pragma unroll
