@@ -13,8 +13,9 @@ K='conv_bwd_data_kernel|conv_fwd_kernel|conv_wgrad_kernel|dense1_bwd_adam_kernel
 CMD="python bench.py --steps 1 --warmup 1 --no-cpu-baseline"
 # the counter passes run without the bench's in-stream HIP events (a --pmc pass with an event record around
 # every launch crashed rocprofv3's counter thread: SIGSEGV, gpurun_out/profile_r02v6/fetch.err) and without
-# the config #4 sub-leg (its kernels are not the roofline kernels)
-PMC="$CMD --no-kernel-timer --no-cifar"
+# the config #4, tutorial and Titanic sub-legs (their MNIST launches at other batch shapes would be averaged into
+# the config #3 kernels' bytes per launch)
+PMC="$CMD --no-kernel-timer --no-cifar --no-tutorial --no-titanic"
 if [ "$2" != "pmc" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/trace -o run --output-format csv -- $CMD > $O/trace.json 2> $O/trace.err || exit $?
   cp $R/trace/run_kernel_stats.csv $O/kernel_stats.csv || exit 40
