@@ -161,7 +161,10 @@ __global__ __launch_bounds__(FWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     int cnt_all, int bmax, const float* __restrict__ params, int64_t stride, const float* __restrict__ U,
     float* __restrict__ pooled, uint8_t* __restrict__ code) {
   __shared__ float img_s[2][FWD_IMR * IMG];  // double-buffered: the next sample's image goes in beside the current
-  __shared__ float a1_s[FWD_C1T * 32 * A1P];  // padded to whole conv1 tiles: unconditional writes (rows >= 260 unread)
+  // padded to whole conv1 tiles: unconditional writes (rows >= 260 unread).  (Its rows padded to 12 (mod 16) floats
+  // - conflict-free patch reads, as conv_bwd_data's - spilled 33 registers: the address arithmetic of the conv1
+  // epilogue, p A1P + 2 (p / 26) per value, round 6)
+  __shared__ float a1_s[FWD_C1T * 32 * A1P];
   __shared__ float t_s[8 * FWD_TQ];  // [i][b][16 tiles][64 co]
   const int64_t lb = xcd_block();  // logical block (part, sample group, r), replica-major
   const int part = (int)(lb % FWD_PARTS);
@@ -1039,7 +1042,11 @@ constexpr int BWD_WR = 7;                      // window rows a band's patches t
 constexpr int BWD_DR = 2 * BWD_WR;             // dZ2 rows staged
 constexpr int BWD_DC = Z2 + 4;                 // dZ2 columns staged: 2 zero columns each side
 constexpr int BWD_CS = 17;                     // channel stride (16 channels of a quarter + 1: bank spread)
-constexpr int BWD_RS = BWD_DC * BWD_CS;        // staged row stride
+// staged row stride, padded to 13 (mod 16): with BWD_CS = 1 (mod 16) tile (tyl, tx) of the 13-wide tile rows starts
+// on bank 2 (13 tyl + tx) = 2 tile (mod 32), so a half-wave's 16 tiles x 2 channels cover the 32 banks once (the
+// unpadded 476 put a group's wrapped tile row on its first row's banks)
+constexpr int BWD_RS = BWD_DC * BWD_CS + (((13 - BWD_DC * BWD_CS) % 16) + 16) % 16;
+static_assert(BWD_CS % 16 == 1 && BWD_RS % 16 == 13, "conflict-free patch reads");
 constexpr int BWD_PAIRS = BWD_WR * PL * 16;    // (dp, code) pairs of a quarter
 constexpr int BWD_PRE = (BWD_PAIRS + BWD_THREADS - 1) / BWD_THREADS;
 constexpr int BWD_UQ = 16 * C1 * 16;           // Ur floats of one channel quarter [co 16][ci 32][xi 16]
@@ -1104,12 +1111,12 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
     // zero columns (2 each side) of every staged row; the interior is rewritten by every quarter
     for (int e = tid; e < BWD_DR * 4 * BWD_CS; e += BWD_THREADS) {
       const int rr = e / (4 * BWD_CS), c = (e / BWD_CS) % 4, k = e % BWD_CS;
-      dz_s[(rr * BWD_DC + (c < 2 ? c : BWD_DC - 4 + c)) * BWD_CS + k] = 0.0f;
+      dz_s[rr * BWD_RS + (c < 2 ? c : BWD_DC - 4 + c) * BWD_CS + k] = 0.0f;
     }
   }
   // A operand (V): this lane's tile tl of the wave's group at channel kq of each k-step
   const int tcl = min(gt0 + tl, BWD_TILES - 1);
-  const int pa = ((2 * (tcl / 13 - ty0)) * BWD_DC + 2 * (tcl % 13)) * BWD_CS + kq;
+  const int pa = (2 * (tcl / 13 - ty0)) * BWD_RS + 2 * (tcl % 13) * BWD_CS + kq;
   // B operand (Ur): ci = 16h + tl, co = 4st + kq of the quarter; chunk m of the 16 transform points at
   // m ^ swz (the staging applies the same XOR)
   const int swz = (tl >> 2) & 3;
@@ -1144,14 +1151,14 @@ __global__ __launch_bounds__(BWD_THREADS) __attribute__((amdgpu_waves_per_eu(2, 
           const uint32_t c = pcd[s];
           const float v = (c & 0x80) ? pdv[s] : 0.0f;
           const int sel = c & 3;
-          float* d = dz_s + ((2 * lwy) * BWD_DC + 2 + 2 * wx) * BWD_CS + ch;
+          float* d = dz_s + (2 * lwy) * BWD_RS + (2 + 2 * wx) * BWD_CS + ch;
           // the window's 4 pixels zeroed, then the value at the argmax (same thread, same address: in order): no
           // per-pixel compare / select chain (SGPR-mask hazards padded with s_nop in every one)
           d[0] = 0.0f;
           d[BWD_CS] = 0.0f;
-          d[BWD_DC * BWD_CS] = 0.0f;
-          d[BWD_DC * BWD_CS + BWD_CS] = 0.0f;
-          d[(sel >> 1) * (BWD_DC * BWD_CS) + (sel & 1) * BWD_CS] = v;
+          d[BWD_RS] = 0.0f;
+          d[BWD_RS + BWD_CS] = 0.0f;
+          d[(sel >> 1) * BWD_RS + (sel & 1) * BWD_CS] = v;
         }
       }
 #endif

@@ -3,7 +3,7 @@ CNN oracle, for tests/test_ranking_gpu.py ("partner ranking i
 exact-Shapley scale north_star names, mplc/contributivity.py:140-171, 1210-1253; tests/end_to_end_tests.py:66-73
 ports the reference's own ranking assertion at 2 partners).
 
-    python scripts/ranking_fixture.py [workers]
+    python scripts/ranking_fixture.py [workers] [threads_per_worker]
 
 The scenario (tests/spread_fixtures.py ranking_scenario, chosen on the GPU with scripts/probe_ranking.py: a partner
 ranking that survives ~1-ulp perturbations of the data with every adjacent gap several times the perturbations'
@@ -31,9 +31,9 @@ for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "distributed-lea
 _STATE = {}
 
 
-def _init():
+def _init(threads=1):
     import torch
-    torch.set_num_threads(1)
+    torch.set_num_threads(threads)
     from oracle import cnn as ocnn
     from spread_fixtures import ranking_scenario
     sc = ranking_scenario()
@@ -54,6 +54,7 @@ def main():
     from oracle import shapley as oshap
     from spread_fixtures import GOLDEN, RANKING, data_crc, ranking_scenario
     workers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    threads = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # another summation order: a second oracle sample
     sc = ranking_scenario()
     n = len(sc.partners_list)
     coals = [c for k in range(1, n + 1) for c in itertools.combinations(range(n), k)]
@@ -61,7 +62,7 @@ def main():
     order = sorted(coals, key=lambda c: -sum(len(sc.partners_list[p].train_idx) for p in c))
     t0 = time.time()
     V = np.zeros(1 << n)
-    with get_context("spawn").Pool(workers, initializer=_init) as pool:
+    with get_context("spawn").Pool(workers, initializer=_init, initargs=(threads,)) as pool:
         for i, (coal, v) in enumerate(pool.imap_unordered(_value, order, chunksize=1)):
             V[sum(1 << p for p in coal)] = v
             if i % 50 == 0:
@@ -73,8 +74,8 @@ def main():
            "partner_rows": [len(p.train_idx) for p in sc.partners_list],
            "batch_sizes": [int(p.batch_size) for p in sc.partners_list],
            "values_bitmask": V.tolist(), "shapley": sv, "argsort": [int(i) for i in np.argsort(sv)],
-           "threads_per_worker": 1, "wall_s": round(time.time() - t0, 1)}
-    path = os.path.join(GOLDEN, "ranking_10p.json")
+           "threads_per_worker": threads, "wall_s": round(time.time() - t0, 1)}
+    path = os.path.join(GOLDEN, "ranking_10p.json" if threads == 1 else f"ranking_10p_t{threads}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", path, "shapley", np.round(sv, 4).tolist(), "argsort", out["argsort"], f"{out['wall_s']}s")
