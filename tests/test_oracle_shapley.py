@@ -58,3 +58,24 @@ def test_efficiency_property_large_n():
     assert abs(sv.sum() - V[-1]) < 1e-13
     sv64 = osh.shapley_bitmask_f64_omp(n, V, threads=4)
     assert np.max(np.abs(sv64 - sv)) < 1e-11 * np.max(np.abs(sv))
+
+
+def test_ranking_fixtures_consistent():
+    """tests/golden/ranking_10p*.json (scripts/ranking_fixture.py, two summation orders of the CNN oracle): the stored
+    Shapley values are the reference-order restatement of the stored v(S) table, and both passes describe the same
+    scenario (tests/test_ranking_gpu.py derives its tie bands from their difference)."""
+    import itertools
+    import json
+    import os
+    import numpy as np
+    from oracle import shapley as oshap
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    recs = [json.load(open(os.path.join(golden, f))) for f in ("ranking_10p.json", "ranking_10p_t2.json")]
+    assert recs[0]["data_crc32"] == recs[1]["data_crc32"] and recs[0]["scenario"] == recs[1]["scenario"]
+    assert [r["threads_per_worker"] for r in recs] == [1, 2]
+    n = len(recs[0]["shapley"])
+    coals = [c for k in range(1, n + 1) for c in itertools.combinations(range(n), k)]
+    for r in recs:
+        v = [r["values_bitmask"][sum(1 << p for p in c)] for c in coals]
+        assert [float(x) for x in oshap.shapley_reference_order(n, v)] == r["shapley"]
+        assert abs(sum(r["shapley"]) - r["values_bitmask"][(1 << n) - 1]) < 1e-12
