@@ -730,7 +730,7 @@ def cpu_baseline_cifar(sc, coalitions, epochs, M):
                        f"linearly in |S|: {total:.0f}s")}
 
 
-CIFAR_TIMER_EVERY = 4  # config #4: the in-stream timer on one lockstep batch in 4 (bench_cifar's progress())
+CIFAR_TIMER_EVERY = 1  # config #4: the in-stream timer on every lockstep batch of the profile pass (bench_cifar)
 CIFAR_SUBLEG_S = 115.0  # one config #4 TMCS run on one MI355X (round-2 measurement: 107 s)
 
 
@@ -755,15 +755,19 @@ def bench_cifar(args, rank, world, sub=False):
     s0 = [0]
     sampled = {"batches": 0, "timed": 0, "timed_replica_steps": 0, "replica_steps": 0}
 
+    prof = {"on": False}
+
     def progress(s, total, R):
-        """Batch start: heartbeat on stderr, and the in-stream timer's batch sampling.  An event record around
-        every launch costs about 15 % of this leg's wall time (its kernels are 40-340 us and a timing event
-        flushes between them), so the timer runs on one lockstep batch in CIFAR_TIMER_EVERY; the kernels
-        table and roofline come from those batches (their own launches and stashed schedules)."""
+        """Batch start: heartbeat on stderr, and in the profile pass the in-stream timer's batch sampling.  An
+        event record around every launch costs about 15 % of this leg's wall time (its kernels are 40-340 us and a
+        timing event flushes between them), and a timed batch runs as ONE lockstep batch on one stream - so the
+        timer runs in a profile pass of the same (deterministic) TMCS job before the timed step, and the timed
+        step runs every batch as the product does (two HIP streams, no events).  The kernels table and roofline
+        come from the profile pass (its own launches and stashed schedules); `value` from the timed step."""
         if s != 0:
             return
         log(f"cifar: batch of {R} replicas, {total} steps, {eng.stats['coalitions']} coalitions so far")
-        if s0[0] == 0 or args.no_kernel_timer:
+        if not prof["on"]:
             return
         on = sampled["batches"] % CIFAR_TIMER_EVERY == 0
         eng.profiler = timer if on else None
@@ -785,18 +789,30 @@ def bench_cifar(args, rank, world, sub=False):
     # launches can be set beside the algorithmic bytes of the same launches (scripts/pmc_traffic.py)
     stash_all = StashOnly(args.cifar_profile_kernel) if args.no_kernel_timer else None
 
+    def profile_step():  # the warm-up: the same job with the in-stream timer on (progress())
+        prof["on"] = not args.no_kernel_timer
+        try:
+            return one_step()
+        finally:
+            prof["on"] = False
+            eng.profiler = None
+
     def timed_step(i, planned):
         if s0[0] == 0:
-            eng.profiler = stash_all  # None: set per lockstep batch by progress()
+            eng.profiler = stash_all  # None (no events in the timed steps) unless counters are being collected
             eng.time_test_eval = True
             s0[0] = eng.stats["samples"] or -1
         return one_step()
 
+    # the profile pass is the warm-up step; without the timer (counter passes) there is none
+    n_warm = 0 if args.no_kernel_timer else 1
     if sub:
-        steps, warm, wall, c, _ = run_budgeted(one_step, timed_step, args, world, 0, "cifar", max_steps=1, warmup=0)
+        steps, warm, wall, c, _ = run_budgeted(profile_step, timed_step, args, world, 0, "cifar", max_steps=1,
+                                               warmup=n_warm)
     else:
         reserve = (60 if (world == 1 and not args.no_cpu_baseline) else 0) + 15
-        steps, warm, wall, c, _ = run_budgeted(one_step, timed_step, args, world, reserve, "cifar")
+        steps, warm, wall, c, _ = run_budgeted(profile_step, timed_step, args, world, reserve, "cifar",
+                                               warmup=max(n_warm, min(args.warmup, 1)))
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
     timer.stash = []
@@ -870,10 +886,10 @@ def bench_cifar(args, rank, world, sub=False):
                          "replica_steps_timed": sampled["timed_replica_steps"],
                          "replica_steps": sampled["replica_steps"],
                          "streams": eng.concurrent_batches,
-                         "note": f"in-stream HIP events around every launch of one lockstep batch in {CIFAR_TIMER_EVERY}, "
-                                 "which runs as ONE batch on one stream (the others in two halves on two HIP streams, "
-                                 "the CIFAR10 default: CnnBatchTrainer.run_concurrent); "
-                                 "value covers the whole run, timed and untimed batches"},
+                         "note": "in-stream HIP events around every launch of every lockstep batch of the profile "
+                                 "pass (the warm-up step: the same deterministic TMCS job), each batch then run as ONE "
+                                 "batch on one stream; the timed step runs without events, every batch in two halves "
+                                 "on two HIP streams (the CIFAR10 default: CnnBatchTrainer.run_concurrent)"},
     }
     # the roofline on the step's dominant kernel (largest share of the kernel time), as the config #3 line
     dom = max((k for k in kernels if "frac" in kernels[k]), key=lambda k: kernels[k]["ms_total"], default=None)
