@@ -744,7 +744,10 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
 // W3 out), and the next round's first step reads W3 from the coalition row (w3src): every replica W3 store of the
 // round's last step and the aggregation's W3 reads disappear.  A member without a step this time (it finished
 // its round's fit earlier: fewer rows) enters with its own row, as the aggregation would read it.
-__global__ __launch_bounds__(256) void dense1_bwd_adam_avg_kernel(
+#ifndef MPLC_D1AVG_WAVES
+#define MPLC_D1AVG_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPLC_D1AVG_WAVES, MPLC_D1AVG_WAVES))) void dense1_bwd_adam_avg_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ adam_t, int bmax, float* __restrict__ params, float* __restrict__ adam_m,
     float* __restrict__ adam_v, int64_t stride, const float* __restrict__ glob, const int32_t* __restrict__ w3src,
