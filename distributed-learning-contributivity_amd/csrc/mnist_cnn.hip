@@ -745,7 +745,10 @@ __global__ __launch_bounds__(256) void dense1_bwd_adam_kernel(
 // round's last step and the aggregation's W3 reads disappear.  A member without a step this time (it finished
 // its round's fit earlier: fewer rows) enters with its own row, as the aggregation would read it.
 #ifndef MPLC_D1AVG_WAVES
-#define MPLC_D1AVG_WAVES 2
+// waves per SIMD: 3 (168 VGPRs, 2 spilled) against the unconstrained 2 (172 VGPRs): 96.7 -> 84.7 ms over the config #3
+// probe's 40 launches, bit-identical (profiles/r06_ab_avgw.txt).  Still ~0.4 of HBM: each block walks its
+// coalition's replicas one after the other (load, stage, reduce, update per replica)
+#define MPLC_D1AVG_WAVES 3
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPLC_D1AVG_WAVES, MPLC_D1AVG_WAVES))) void dense1_bwd_adam_avg_kernel(
     const float* __restrict__ Pool, const float* __restrict__ dH, const int32_t* __restrict__ cnt,
