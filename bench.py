@@ -98,6 +98,35 @@ def kernel_table(timer, units):
     return out
 
 
+def dense1_split(eng, timer):
+    """The dense1_bwd_adam entry over its two kinds of step (ABI 4): the steps without the fused W3 average (one
+    dense pass per replica) and a FedAvg round's last step (dense1_bwd_adam_kernel for the replicas outside fused
+    coalitions + dense1_bwd_adam_avg_kernel, timed between the same two events).  Per launch ms from the in-stream
+    timer in step order, beside each step's own algorithmic bytes (MnistModel.algorithmic_units of its stash
+    record)."""
+    ms = timer.per.get("dense1_bwd_adam", [])
+    recs = timer.stash
+    if not ms or len(ms) != len(recs):
+        return None
+    acc = {"unfused_steps": [0, 0.0, 0.0], "fused_steps": [0, 0.0, 0.0]}
+    for t, rec in zip(ms, recs):
+        fused = len(rec) > 3 and bool((rec[3] > 0).any().item())
+        e = acc["fused_steps" if fused else "unfused_steps"]
+        e[0] += 1
+        e[1] += t
+        e[2] += eng.model_impl.algorithmic_units([rec])["dense1_bwd_adam_bytes"]
+    out = {}
+    for k, (n, t, b) in acc.items():
+        if n:
+            rate = b / (t / 1000) / 1e9
+            out[k] = {"launches": n, "ms_avg": round(t / n, 4), "achieved": round(rate, 2), "unit": "GB/s",
+                      "frac": round(rate / HBM_PEAK_GBS, 4), "bytes_per_launch": int(b / n)}
+    out["note"] = ("a FedAvg round's last step runs the fused W3 average (dense1_bwd_adam_avg_kernel: each block walks "
+                   "its coalition's replicas in turn) in place of the replicas' W3 stores and the aggregation's W3 "
+                   "reads; the entry above covers both kinds of step")
+    return out
+
+
 TRAFFIC_SOURCE = ("profiles/pmc_traffic.json: FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes of "
                   "this same command (scripts/pmc_traffic.py), not measured in this run")
 
@@ -538,7 +567,7 @@ def bench_train(args, rank, world):
         c.compute_contributivity("Shapley values")
         return c
 
-    timer = KernelTimer("all", TRAIN_KERNELS, stash=True)
+    timer = KernelTimer("all", TRAIN_KERNELS, stash=True, per_launch=("dense1_bwd_adam",))
     reps0 = [None]
     n_on = [0]
 
@@ -565,8 +594,11 @@ def bench_train(args, rank, world):
     steps, warm, wall, c, per_step = run_budgeted(one_step, timed_step, args, world, reserve, "train")
     eng.profiler = None
     units = eng.model_impl.algorithmic_units(timer.stash)
-    timer.stash = []
     kernels = kernel_table(timer, units)
+    split = dense1_split(eng, timer)
+    if split:
+        kernels["dense1_bwd_adam"]["split"] = split
+    timer.stash = []
     local_reps = eng.stats["replicas"] - reps0[0]
     samples = units.get("samples", 0.0) / max(1, n_on[0]) * steps  # the stash covers the timer-on steps
     ms_per_step = wall * 1000 / steps

@@ -15,9 +15,10 @@ PROF_ALL = -1  # include/mplc_hip_cnn.h MPLC_PROF_ALL
 
 
 class KernelTimer:
-    def __init__(self, kernel, names=None, stash=False):
+    def __init__(self, kernel, names=None, stash=False, per_launch=()):
         self.kernel = kernel
         self.want_stash = stash
+        self.per = {n: [] for n in per_launch}  # every launch's ms, in launch order, for these kernel names
         self.names = list(names) if names is not None else [kernel]
         self.pending = []            # [(name, begin, end)]
         self.ms = {n: 0.0 for n in self.names}
@@ -44,8 +45,11 @@ class KernelTimer:
         for name, a, b in self.pending:
             if block or b.query():
                 if name in self.ms:
-                    self.ms[name] += a.elapsed_time(b)
+                    ms = a.elapsed_time(b)
+                    self.ms[name] += ms
                     self.count[name] += 1
+                    if name in self.per:
+                        self.per[name].append(ms)
             else:
                 keep.append((name, a, b))
         self.pending = keep
